@@ -1,0 +1,175 @@
+/*
+ * mpct.h — C ABI of the MI355X batched closed-loop GPC scoring engine (libmpct.so).
+ *
+ * Drop-in boundary for the reference's per-candidate closed-loop seam
+ *   function [y,u,t,ys,uopt] = closedloop_toolbox(mpc_toolbox,r,v,N,Nu,delta,lambda,nit)
+ *   (MPC-Tuning/MPC_Tuning/closedloop_toolbox.m:1), called once per candidate (and once per
+ *   output for square plants) by VNS2.m:153,168 and GAM_fun.m:81.
+ * Here one call scores a whole BATCH of candidates (N2, Nu, delta, lambda) on the GPU.  A
+ * MATLAB host binds it with loadlibrary('libmpct','mpct.h') / calllib, or through the MEX
+ * shim in INTEGRATION.md; the Python host mirror (mpct/) binds it with ctypes.
+ *
+ * Conventions
+ *   - plain C types only; every matrix is row-major double; "row signals" are [row][t].
+ *   - the caller owns every input/output buffer; the library owns the scenario (host tables
+ *     and their device copies) until mpct_scenario_destroy.
+ *   - negative return codes are argument / shape / device errors (message in
+ *     mpct_last_error(), thread-local); per-candidate numerical trouble never fails the call:
+ *     it is reported in mpct_result.status[] with NaN costs (the reference swallows such
+ *     errors with fprintf and continues: VNS2.m:161-163, GAM_fun.m:191-193).
+ *   - threading: one scenario per host thread, or external synchronisation.  All device work
+ *     of a call is complete when mpct_eval_batch returns.
+ */
+#ifndef MPCT_H
+#define MPCT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCT_ABI_VERSION 1
+
+/* error codes */
+#define MPCT_OK 0
+#define MPCT_EINVAL (-1)   /* bad argument / shape                                  */
+#define MPCT_ENOMEM (-2)   /* host or device allocation failed                      */
+#define MPCT_EDEVICE (-3)  /* HIP runtime error (no device, launch failure, ...)    */
+#define MPCT_ERANGE (-4)   /* a size exceeds what the compiled kernels support       */
+
+/* per-simulation status bits (mpct_result.status) */
+#define MPCT_ST_OK 0
+#define MPCT_ST_QP_MAXITER 1   /* active-set iteration cap hit at some step          */
+#define MPCT_ST_QP_INFEAS 2    /* QP infeasible at some step (dual unbounded)        */
+#define MPCT_ST_NONFINITE 4    /* a non-finite value appeared in the state           */
+#define MPCT_ST_SKIPPED 8      /* padding / sentinel candidate (N2 <= 0)             */
+#define MPCT_ST_BADHORIZON 16  /* N2/Nu outside the scenario's range or Nu > N2      */
+
+/* One SISO discrete transfer function  y = z^-delay * num(z)/den(z) u  in the form tfdata(.,'v')
+ * returns it (descending powers of z, numerator padded to the denominator's length, den[0]=1)
+ * — the representation descompMPC.m:194 reads.  len = number of coefficients of each. */
+typedef struct mpct_dtf {
+  int32_t len;
+  const double* num;
+  const double* den;
+  int32_t delay;
+} mpct_dtf;
+
+/* Scenario: everything that does not depend on the candidate.
+ *   plant[i*(nu+nd)+j]  : simulated plant entries (the toolbox's sim simulates the model
+ *                         itself unless options.Model is set: closedloop_toolbox.m:50)
+ *   model[i*(nu+nd)+j]  : prediction model entries, used for the MatG step responses
+ *                         (MatG.m:51 step(Ps(i,j),...))
+ *   carima_A / carima_B : the CARIMA form after descompMPC + BA_MIMO (DTC_GPC_WW.m:79):
+ *                         A_i (na[i]+1 coeffs, z^-1 powers, A_i[0]=1) concatenated over i;
+ *                         B_ij (nb[i*(nu+nd)+j]+1 coeffs) concatenated row-major over (i,j);
+ *                         dp[i*(nu+nd)+j] the descompMPC delays.
+ *   n1[i]               : first predicted step of output i: 1 = toolbox window t+1..t+N2
+ *                         (PredictionHorizon semantics), dmin_i+1 = GPC window (MatG.m:64,
+ *                         diophantine.m:44 N1 = d+1)
+ *   weights_squared     : 1 = toolbox cost (Weights enter squared), 0 = DTC_GPC_WW.m:67-76
+ *   du_min..u_max[nu]   : MV rate / amplitude bounds (already scaled, MPCTuning.m:170-178);
+ *                         +-INFINITY disables a bound
+ *   n2_max, nu_max      : largest horizons any candidate of this scenario may use
+ *   nit                 : closed-loop length (Par.nit);  vns_ink: VNS2.m:43 inK (1-based)
+ *   yref[my*nit]        : GAM/VNS reference trajectory Par.Yref (MPCTuning.m:188,320)      */
+typedef struct mpct_scenario_desc {
+  int32_t abi_version; /* = MPCT_ABI_VERSION */
+  int32_t my, nu, nd;
+  int32_t nit;
+  int32_t n2_max, nu_max;
+  int32_t weights_squared;
+  int32_t vns_ink;
+  const int32_t* n1;
+  const mpct_dtf* plant;
+  const mpct_dtf* model;
+  const int32_t* na;
+  const double* carima_A;
+  const int32_t* nb;
+  const double* carima_B;
+  const int32_t* dp;
+  const double* du_min;
+  const double* du_max;
+  const double* u_min;
+  const double* u_max;
+  const double* yref;
+} mpct_scenario_desc;
+
+typedef struct mpct_scenario mpct_scenario;
+
+/* Evaluation options. */
+typedef struct mpct_opts {
+  int32_t open_loop;   /* 1: also compute the open-loop first-move prediction (uopt, ys) and
+                          the VNS terms j21/Jnu (closedloop_toolbox.m:85-100); 0: closed loop
+                          + J1/j22 only (all GAM_fun needs, GAM_fun.m:81)                  */
+  int32_t want_traj;   /* 1: write y/u (and ys/uopt if open_loop) trajectories             */
+  int32_t max_qp_iter; /* active-set iteration cap per step (0 = default 8*M)              */
+  int32_t device;      /* HIP device ordinal (-1 = current)                               */
+  double feas_tol;     /* constraint feasibility tolerance (0 = default 1e-10)            */
+} mpct_opts;
+
+/* Results, one row per SIMULATION s = c*nref + k (candidate c, reference k).  Any pointer may
+ * be NULL to skip that output.  Sizes: J1/j21/j22 [S*my], Jnu [S*nu], status/qp_iters [S],
+ * y/ys [S*my*nit], u/uopt [S*nu*nit].
+ *   J1[i]  = sum_t (y_i - yref_i)^2                       GAM_fun.m:219-220
+ *   j21[i] = sum_{t>=inK} (y_i - ys_i)^2                   VNS2.m:172,176
+ *   j22[i] = sum_{t>=inK} (y_i - yref_i)^2                 VNS2.m:173,177
+ *   Jnu[n] = sum_t (|uopt_n(1)| / |diff(uopt_n)|)^2, inf/NaN -> 0   VNS2.m:183-191           */
+typedef struct mpct_result {
+  double* J1;
+  double* j21;
+  double* j22;
+  double* Jnu;
+  int32_t* status;
+  int64_t* qp_iters;
+  double* y;
+  double* u;
+  double* ys;
+  double* uopt;
+} mpct_result;
+
+/* Version / capability query (no device needed). */
+int32_t mpct_abi_version(void);
+const char* mpct_last_error(void);
+
+/* Build a scenario: validates the description, precomputes the candidate-independent tables on
+ * the host (step responses s_ij(t), Diophantine F rows, deltaUFree/cell2mat2 past-control
+ * rows; see DESIGN.md §Data layout).  Does NOT touch the GPU (device copies are made on first
+ * evaluation), so it is usable on a CPU-only host for inspection.  Returns MPCT_OK. */
+int32_t mpct_scenario_create(const mpct_scenario_desc* desc, mpct_scenario** out);
+void mpct_scenario_destroy(mpct_scenario* s);
+
+/* Host-table inspection (testing / MATLAB-side debugging; no device needed).
+ *   which: 0 = MV step table [my][nu][tlen], 1 = free-response table Phi [my*n2_max][nx],
+ *          2 = dims {my, nu, nd, n2_max, nu_max, tlen, nx, nyh, nup},
+ *          3 = Phi on the device state basis [y-r, backward differences of y | du history]
+ * Copies at most cap doubles into buf; returns the number of doubles the table holds, or <0. */
+int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, double* buf, int64_t cap);
+
+/* Score C candidates x nref references.  Host pointers (MATLAB / ctypes callers).
+ *   N2[C], Nu[C]      horizons used by the toolbox: max(N), max(Nu) (closedloop_toolbox.m:38-40)
+ *   delta[C*my], lambda[C*nu]   Weights.OV, Weights.MVRate (closedloop_toolbox.m:42-43)
+ *   r[nref*my*nit]    reference sets (row signals; VNS passes one unit step per output,
+ *                     VNS2.m:148-150; GAM passes Xsp)
+ *   v[nref*nd*nit]    measured disturbances per reference set (may be NULL when nd == 0)  */
+int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                        const double* delta, const double* lambda, int32_t nref, const double* r,
+                        const double* v, const mpct_opts* opts, mpct_result* out);
+
+/* Same, all pointers DEVICE pointers (inputs already resident in HBM; results written to
+ * device memory), enqueued on `stream` (a hipStream_t, NULL = default stream) and NOT
+ * synchronised — the caller synchronises.  Used by multi-GPU sharding and the benchmark. */
+int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                               const double* delta, const double* lambda, int32_t nref,
+                               const double* r, const double* v, const mpct_opts* opts,
+                               mpct_result* out, void* stream);
+
+/* Bytes of dynamic LDS one simulation's workgroup uses for this scenario at (N2, Nu); <0 on
+ * error.  Lets a host check occupancy before launching. */
+int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCT_H */

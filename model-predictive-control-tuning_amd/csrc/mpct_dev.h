@@ -1,0 +1,58 @@
+// mpct_dev.h — device-side scenario layout shared by the host precompute (mpct_host.cpp) and
+// the closed-loop kernel (gpc_kernel.hip).  Plain POD passed by value as a kernel argument.
+#pragma once
+#include <stdint.h>
+
+namespace mpct {
+
+constexpr int kMaxOut = 16;    // outputs (my)
+constexpr int kMaxIn = 16;     // inputs (nu + nd)
+constexpr int kURing = 64;     // plant input history ring (power of two)
+constexpr int kYeHist = 8;     // plant entry output history ring (power of two)
+constexpr int kWave = 64;
+
+// per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
+constexpr int MPCT_ST_QP_MAXITER_ = 1;
+constexpr int MPCT_ST_QP_INFEAS_ = 2;
+constexpr int MPCT_ST_NONFINITE_ = 4;
+constexpr int MPCT_ST_SKIPPED_ = 8;
+constexpr int MPCT_ST_BADHORIZON_ = 16;
+
+struct DevScenario {
+  int my, nu, nd, nin, nit;
+  int n2max, numax, tlen;   // step table length per entry
+  int nx;                   // free-response state: [y histories | du histories]
+  int nyh, nup;             // sizes of the two parts
+  int wsq;                  // weights squared
+  int ink0;                 // VNS inK, 0-based
+  int ne;                   // plant entries my*nin
+  int pl_maxb, pl_maxa;     // longest plant numerator (incl. delay) / denominator
+  // tables (device pointers into one allocation)
+  const double* step;   // [my][nu][tlen]   model step responses s_ij(t), t = 0..tlen-1
+  const double* phi;    // [my*n2max][nx]   free response rows (Diophantine F | deltaUFree Hp)
+  const int* n1;        // [my]   first predicted step
+  const int* yoff;      // [my]   offset of y_i history (length na_i+1) in the state
+  const int* nyhi;      // [my]   na_i + 1
+  const int* upoff;     // [nu]   offset of du_n history (length duM_n) in the state
+  const int* dum;       // [nu]   duM_n
+  const int* pl_nb;     // [ne]   plant entry numerator length (z^-1, delay folded in)
+  const int* pl_na;     // [ne]   plant entry denominator length
+  const double* pl_b;   // [ne][pl_maxb]
+  const double* pl_a;   // [ne][pl_maxa]
+  const double* bnd;    // [4][nu]  du_min, du_max, u_min, u_max
+  const double* yref;   // [my][nit]
+};
+
+struct DevOpts {
+  int open_loop, want_traj, max_qp_iter;
+  double feas_tol;
+};
+
+struct DevResult {
+  double *J1, *j21, *j22, *Jnu;
+  int32_t* status;
+  int64_t* qp_iters;
+  double *y, *u, *ys, *uopt;
+};
+
+}  // namespace mpct

@@ -1,0 +1,556 @@
+// mpct_host.cpp — C ABI of libmpct: scenario validation, host precompute of the candidate-
+// independent GPC tables, device upload, launch wrappers.  See include/mpct.h.
+//
+// Host tables (restating the reference's setup functions, natively):
+//   step[i][n][t]     step response of model entry (i,n), t = 0..tlen-1      (MatG.m:51 step)
+//   F_i rows          Diophantine free-output polynomials for the window      (diophantine.m:35-65)
+//   uG_in rows        past-control coefficients, ALL zeros removed, last cp    (deltaUFree.m:13-62)
+//   phi[(i,r)][s]     = [F_i row r | uG_i* row r] laid out on the state vector
+//                       x = [y_1(t..t-na_1) ... | du_1(t-1..t-duM_1) ...]     (cell2mat2.m,
+//                       DTC_GPC_WW.m:139-146: yf = Hp*up + S*Yd)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mpct.h"
+#include "mpct_dev.h"
+
+namespace mpct {
+// defined in gpc_kernel_launch.hip
+int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
+                       const double* delta, const double* lambda, const double* r,
+                       const double* v, const DevOpts& o, const DevResult& out, int maxM,
+                       hipStream_t stream, std::string* err);
+long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
+}  // namespace mpct
+
+using namespace mpct;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct mpct_scenario {
+  int my = 0, nu = 0, nd = 0, nin = 0, nit = 0, n2max = 0, numax = 0, wsq = 1, ink0 = 9;
+  std::vector<int> n1;
+  int tlen = 0;
+  std::vector<double> step;  // [my][nu][tlen]
+  int nx = 0, nyh = 0, nup = 0;
+  std::vector<int> yoff, nyhi, upoff, dum;
+  std::vector<double> phi;   // [my*n2max][nx]  reference layout (S | Hp)
+  std::vector<double> phid;  // same rows on the device state basis (see create)
+  int ne = 0, pl_maxb = 0, pl_maxa = 0;
+  std::vector<int> pl_nb, pl_na;
+  std::vector<double> pl_b, pl_a;
+  std::vector<double> bnd;   // [4][nu]
+  std::vector<double> yref;  // [my][nit]
+  // device state
+  int dev = -2;
+  void* dtab = nullptr;
+  DevScenario ds{};
+  // scratch buffers for the host-pointer API (grow only)
+  void* dscratch = nullptr;
+  size_t dscratch_bytes = 0;
+};
+
+extern "C" int32_t mpct_abi_version(void) { return MPCT_ABI_VERSION; }
+extern "C" const char* mpct_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------
+static std::vector<double> conv(const std::vector<double>& a, const std::vector<double>& b) {
+  if (a.empty() || b.empty()) return {};
+  std::vector<double> c(a.size() + b.size() - 1, 0.0);
+  for (size_t i = 0; i < a.size(); ++i)
+    for (size_t j = 0; j < b.size(); ++j) c[i + j] += a[i] * b[j];
+  return c;
+}
+
+// direct-form discrete filter of a unit step: z^-delay num(z)/den(z) (tfdata form)
+static void step_response(const mpct_dtf& d, int T, double* s) {
+  const int len = d.len;
+  std::vector<double> b(d.delay + len, 0.0), a(len);
+  for (int k = 0; k < len; ++k) {
+    b[d.delay + k] = d.num[k] / d.den[0];
+    a[k] = d.den[k] / d.den[0];
+  }
+  std::vector<double> y(T, 0.0);
+  for (int t = 0; t < T; ++t) {
+    double acc = 0.0;
+    for (int l = 0; l < (int)b.size(); ++l)
+      if (t - l >= 0) acc += b[l];  // unit step input
+    for (int l = 1; l < len; ++l)
+      if (t - l >= 0) acc -= a[l] * y[t - l];
+    y[t] = acc;
+  }
+  std::copy(y.begin(), y.end(), s);
+}
+
+extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenario** out) {
+  if (!d || !out) return fail(MPCT_EINVAL, "null argument");
+  *out = nullptr;
+  if (d->abi_version != MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
+  if (d->my < 1 || d->nu < 1 || d->nd < 0 || d->nit < 1 || d->n2_max < 1 || d->nu_max < 1)
+    return fail(MPCT_EINVAL, "non-positive dimension");
+  if (d->my > kMaxOut || d->nu + d->nd > kMaxIn) return fail(MPCT_ERANGE, "too many outputs/inputs");
+  if (d->nd > 0)
+    return fail(MPCT_ERANGE, "measured disturbances (nd > 0) are not supported by this build yet");
+  if (d->nu * d->nu_max > 64) return fail(MPCT_ERANGE, "nu*nu_max > 64 (one wavefront of QP rows)");
+  if (!d->n1 || !d->plant || !d->model || !d->na || !d->carima_A || !d->nb || !d->carima_B || !d->dp ||
+      !d->du_min || !d->du_max || !d->u_min || !d->u_max || !d->yref)
+    return fail(MPCT_EINVAL, "null table pointer");
+  auto* s = new mpct_scenario();
+  s->my = d->my;
+  s->nu = d->nu;
+  s->nd = d->nd;
+  s->nin = d->nu + d->nd;
+  s->nit = d->nit;
+  s->n2max = d->n2_max;
+  s->numax = d->nu_max;
+  s->wsq = d->weights_squared ? 1 : 0;
+  s->ink0 = d->vns_ink - 1;
+  const int my = s->my, nu = s->nu, nin = s->nin, N = s->n2max;
+  s->n1.assign(d->n1, d->n1 + my);
+  int n1max = 0;
+  for (int i = 0; i < my; ++i) {
+    if (s->n1[i] < 1) {
+      delete s;
+      return fail(MPCT_EINVAL, "n1[i] must be >= 1");
+    }
+    n1max = std::max(n1max, s->n1[i]);
+  }
+  // ---- step table (MatG.m:51): enough samples for s(n1 + r - c), r < n2max
+  s->tlen = n1max + N;
+  s->step.assign((size_t)my * nu * s->tlen, 0.0);
+  for (int i = 0; i < my; ++i)
+    for (int n = 0; n < nu; ++n) {
+      const mpct_dtf& m = d->model[i * nin + n];
+      if (m.len < 1 || !m.num || !m.den || m.den[0] == 0.0 || m.delay < 0) {
+        delete s;
+        return fail(MPCT_EINVAL, "bad model entry");
+      }
+      step_response(m, s->tlen, &s->step[((size_t)i * nu + n) * s->tlen]);
+    }
+  // ---- CARIMA offsets
+  std::vector<int> aoff(my + 1, 0), boff(my * nin + 1, 0);
+  for (int i = 0; i < my; ++i) {
+    if (d->na[i] < 0) {
+      delete s;
+      return fail(MPCT_EINVAL, "na < 0");
+    }
+    aoff[i + 1] = aoff[i] + d->na[i] + 1;
+  }
+  for (int e = 0; e < my * nin; ++e) {
+    if (d->nb[e] < 0 || d->dp[e] < 0) {
+      delete s;
+      return fail(MPCT_EINVAL, "nb/dp < 0");
+    }
+    boff[e + 1] = boff[e] + d->nb[e] + 1;
+  }
+  // ---- state layout
+  s->yoff.resize(my);
+  s->nyhi.resize(my);
+  int o = 0;
+  for (int i = 0; i < my; ++i) {
+    s->yoff[i] = o;
+    s->nyhi[i] = d->na[i] + 1;
+    o += d->na[i] + 1;
+  }
+  s->nyh = o;
+  // cp(i,n) = dp + length(B) - 1  (deltaUFree.m:288-292)
+  std::vector<int> cp(my * nu);
+  s->dum.assign(nu, 0);
+  for (int i = 0; i < my; ++i)
+    for (int n = 0; n < nu; ++n) {
+      int c = d->dp[i * nin + n] + (d->nb[i * nin + n] + 1) - 1;
+      if (c < 1) c = 1;
+      cp[i * nu + n] = c;
+      s->dum[n] = std::max(s->dum[n], c);
+    }
+  s->upoff.resize(nu);
+  for (int n = 0; n < nu; ++n) {
+    s->upoff[n] = o;
+    o += s->dum[n];
+  }
+  s->nx = o;
+  s->nup = o - s->nyh;
+  if (s->nx + my > 256) {
+    delete s;
+    return fail(MPCT_ERANGE, "free-response state too large");
+  }
+  // ---- Diophantine + deltaUFree per output (window rows j = n1_i .. n1_i + N - 1)
+  s->phi.assign((size_t)my * N * s->nx, 0.0);
+  for (int i = 0; i < my; ++i) {
+    const int na = d->na[i];
+    const double* A = d->carima_A + aoff[i];
+    if (A[0] != 1.0) {
+      delete s;
+      return fail(MPCT_EINVAL, "carima_A[i][0] must be 1");
+    }
+    const int dd = s->n1[i] - 1;  // diophantine(A, N, d): N1 = d+1
+    std::vector<double> Ai(A, A + na + 1);
+    std::vector<double> AD = conv(Ai, {1.0, -1.0});  // A~ = A*Delta (diophantine.m:35)
+    const int nAD = (int)AD.size();                 // na + 2
+    const int rows = dd + N + 1;
+    std::vector<double> f((size_t)rows * (nAD - 1), 0.0);
+    auto F = [&](int j, int k) -> double& { return f[(size_t)j * (nAD - 1) + k]; };
+    F(0, 0) = 1.0;
+    for (int j = 0; j < dd + N; ++j) {  // diophantine.m:55-63
+      for (int k = 0; k < nAD - 2; ++k) F(j + 1, k) = F(j, k + 1) - F(j, 0) * AD[k + 1];
+      F(j + 1, nAD - 2) = -F(j, 0) * AD[nAD - 1];
+    }
+    for (int r = 0; r < N; ++r) {
+      const int j = dd + 1 + r;  // prediction step of this row (1-based)
+      double* prow = &s->phi[((size_t)i * N + r) * s->nx];
+      for (int k = 0; k <= na; ++k) prow[s->yoff[i] + k] = F(j, k);
+      // E_j = [1, f(1,0), ..., f(j-1,0)]  (diophantine.m:69-77)
+      std::vector<double> E(j);
+      E[0] = 1.0;
+      for (int k = 1; k < j; ++k) E[k] = F(k, 0);
+      for (int n = 0; n < nu; ++n) {
+        const int e = i * nin + n;
+        std::vector<double> B(d->carima_B + boff[e], d->carima_B + boff[e + 1]);
+        std::vector<double> aux = conv(E, B);
+        std::vector<double> BE;
+        for (double v : aux)
+          if (v != 0.0) BE.push_back(v);  // deltaUFree.m:302-308: every zero removed
+        const int c = cp[i * nu + n];
+        const int lBE = (int)BE.size();
+        double* dst = prow + s->upoff[n];  // left-aligned block (cell2mat2.m:275)
+        if (lBE < c) {
+          for (int k = 0; k < c - lBE; ++k) dst[k] = 0.0;
+          for (int k = 0; k < lBE; ++k) dst[c - lBE + k] = BE[k];
+        } else {
+          for (int k = 0; k < c; ++k) dst[k] = BE[lBE - c + k];
+        }
+      }
+    }
+  }
+  // ---- device copy of phi in a well-conditioned basis.  The F rows have
+  // large alternating coefficients (|F| ~ 3e3 for Shell 3x3) that cancel on the slowly varying
+  // y history; folded into the gain matrix they amplify rounding ~1e4x.  Rewrite the y part on
+  // backward differences, y(t-l) = sum_k (-1)^k C(l,k) nabla^k y(t), and use the identity
+  // F_j(1) = 1 (Atilde(1) = 0 in 1 = E_j Atilde + z^-j F_j) to make the nabla^0 column exactly
+  // 1: the device state is [y_i(t) - r_i(t), nabla y_i(t), ..., nabla^na y_i(t) | du history].
+  s->phid = s->phi;
+  for (int i = 0; i < my; ++i) {
+    const int n = d->na[i] + 1;
+    std::vector<double> binom((size_t)n * n, 0.0);
+    for (int l = 0; l < n; ++l) {
+      binom[(size_t)l * n] = 1.0;
+      for (int k = 1; k <= l; ++k) binom[(size_t)l * n + k] = binom[(size_t)(l - 1) * n + k - 1] +
+                                                           (k <= l - 1 ? binom[(size_t)(l - 1) * n + k] : 0.0);
+    }
+    for (int r = 0; r < N; ++r) {
+      const double* src = &s->phi[((size_t)i * N + r) * s->nx + s->yoff[i]];
+      double* dst = &s->phid[((size_t)i * N + r) * s->nx + s->yoff[i]];
+      for (int k = 0; k < n; ++k) {
+        double a = 0.0;
+        for (int l = k; l < n; ++l) a += src[l] * ((k & 1) ? -binom[(size_t)l * n + k] : binom[(size_t)l * n + k]);
+        dst[k] = a;
+      }
+      dst[0] = 1.0;
+    }
+  }
+  // ---- plant entries in z^-1 form (delay folded into b)
+  s->ne = my * nin;
+  s->pl_nb.resize(s->ne);
+  s->pl_na.resize(s->ne);
+  for (int e = 0; e < s->ne; ++e) {
+    const mpct_dtf& p = d->plant[e];
+    if (p.len < 1 || !p.num || !p.den || p.den[0] == 0.0 || p.delay < 0) {
+      delete s;
+      return fail(MPCT_EINVAL, "bad plant entry");
+    }
+    s->pl_nb[e] = p.delay + p.len;
+    s->pl_na[e] = p.len;
+    s->pl_maxb = std::max(s->pl_maxb, s->pl_nb[e]);
+    s->pl_maxa = std::max(s->pl_maxa, s->pl_na[e]);
+    const int j = e % nin;
+    if (j < nu && p.delay == 0 && p.num[0] != 0.0) {
+      delete s;
+      return fail(MPCT_EINVAL, "plant has direct feedthrough from an MV (algebraic loop)");
+    }
+  }
+  if (s->pl_maxb > kURing || s->pl_maxa > kYeHist) {
+    delete s;
+    return fail(MPCT_ERANGE, "plant entry too long for the device history rings");
+  }
+  s->pl_b.assign((size_t)s->ne * s->pl_maxb, 0.0);
+  s->pl_a.assign((size_t)s->ne * s->pl_maxa, 0.0);
+  for (int e = 0; e < s->ne; ++e) {
+    const mpct_dtf& p = d->plant[e];
+    for (int k = 0; k < p.len; ++k) {
+      s->pl_b[(size_t)e * s->pl_maxb + p.delay + k] = p.num[k] / p.den[0];
+      s->pl_a[(size_t)e * s->pl_maxa + k] = p.den[k] / p.den[0];
+    }
+  }
+  s->bnd.resize(4 * nu);
+  for (int n = 0; n < nu; ++n) {
+    s->bnd[n] = d->du_min[n];
+    s->bnd[nu + n] = d->du_max[n];
+    s->bnd[2 * nu + n] = d->u_min[n];
+    s->bnd[3 * nu + n] = d->u_max[n];
+    if (!(s->bnd[n] <= 0.0 && s->bnd[nu + n] >= 0.0 && s->bnd[2 * nu + n] <= 0.0 &&
+          s->bnd[3 * nu + n] >= 0.0)) {
+      delete s;
+      return fail(MPCT_EINVAL, "bounds must contain 0 (nominal u = 0 must be feasible)");
+    }
+  }
+  s->yref.assign(d->yref, d->yref + (size_t)my * s->nit);
+  *out = s;
+  g_err.clear();
+  return MPCT_OK;
+}
+
+extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
+  if (!s) return;
+  if (s->dtab || s->dscratch) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && s->dev >= 0) (void)hipSetDevice(s->dev);
+    if (s->dtab) (void)hipFree(s->dtab);
+    if (s->dscratch) (void)hipFree(s->dscratch);
+    if (cur >= 0) (void)hipSetDevice(cur);
+  }
+  delete s;
+}
+
+extern "C" int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, double* buf, int64_t cap) {
+  if (!s) return fail(MPCT_EINVAL, "null scenario");
+  std::vector<double> dims;
+  const std::vector<double>* src = nullptr;
+  if (which == 0)
+    src = &s->step;
+  else if (which == 1)
+    src = &s->phi;
+  else if (which == 3)
+    src = &s->phid;
+  else if (which == 2) {
+    dims = {(double)s->my, (double)s->nu, (double)s->nd, (double)s->n2max, (double)s->numax,
+            (double)s->tlen, (double)s->nx, (double)s->nyh, (double)s->nup};
+    src = &dims;
+  } else
+    return fail(MPCT_EINVAL, "unknown table");
+  int64_t n = (int64_t)src->size();
+  if (buf && cap > 0) std::memcpy(buf, src->data(), sizeof(double) * (size_t)std::min<int64_t>(n, cap));
+  return n;
+}
+
+// ------------------------------------------------------------------------------------------
+static int ensure_device(mpct_scenario* s, int want_dev) {
+  int dev = want_dev;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
+  }
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) return fail(MPCT_EDEVICE, "no HIP device");
+  if (dev >= cnt) return fail(MPCT_EINVAL, "device ordinal out of range");
+  if (hipSetDevice(dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipSetDevice failed");
+  if (s->dev == dev && s->dtab) return MPCT_OK;
+  if (s->dtab) {
+    (void)hipFree(s->dtab);
+    s->dtab = nullptr;
+  }
+  if (s->dscratch) {
+    (void)hipFree(s->dscratch);
+    s->dscratch = nullptr;
+    s->dscratch_bytes = 0;
+  }
+  // pack all tables into one allocation, 256-B aligned pieces
+  std::vector<char> blob;
+  auto put = [&](const void* p, size_t bytes) -> size_t {
+    size_t off = (blob.size() + 255) & ~(size_t)255;
+    blob.resize(off + bytes);
+    if (bytes) std::memcpy(blob.data() + off, p, bytes);
+    return off;
+  };
+  size_t o_step = put(s->step.data(), s->step.size() * 8);
+  size_t o_phi = put(s->phid.data(), s->phid.size() * 8);
+  size_t o_n1 = put(s->n1.data(), s->n1.size() * 4);
+  size_t o_yoff = put(s->yoff.data(), s->yoff.size() * 4);
+  size_t o_nyhi = put(s->nyhi.data(), s->nyhi.size() * 4);
+  size_t o_upoff = put(s->upoff.data(), s->upoff.size() * 4);
+  size_t o_dum = put(s->dum.data(), s->dum.size() * 4);
+  size_t o_plnb = put(s->pl_nb.data(), s->pl_nb.size() * 4);
+  size_t o_plna = put(s->pl_na.data(), s->pl_na.size() * 4);
+  size_t o_plb = put(s->pl_b.data(), s->pl_b.size() * 8);
+  size_t o_pla = put(s->pl_a.data(), s->pl_a.size() * 8);
+  size_t o_bnd = put(s->bnd.data(), s->bnd.size() * 8);
+  size_t o_yref = put(s->yref.data(), s->yref.size() * 8);
+  void* dp = nullptr;
+  if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
+  if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(dp);
+    return fail(MPCT_EDEVICE, "hipMemcpy(tables) failed");
+  }
+  char* b = static_cast<char*>(dp);
+  DevScenario& ds = s->ds;
+  ds.my = s->my;
+  ds.nu = s->nu;
+  ds.nd = s->nd;
+  ds.nin = s->nin;
+  ds.nit = s->nit;
+  ds.n2max = s->n2max;
+  ds.numax = s->numax;
+  ds.tlen = s->tlen;
+  ds.nx = s->nx;
+  ds.nyh = s->nyh;
+  ds.nup = s->nup;
+  ds.wsq = s->wsq;
+  ds.ink0 = s->ink0;
+  ds.ne = s->ne;
+  ds.pl_maxb = s->pl_maxb;
+  ds.pl_maxa = s->pl_maxa;
+  ds.step = reinterpret_cast<const double*>(b + o_step);
+  ds.phi = reinterpret_cast<const double*>(b + o_phi);
+  ds.n1 = reinterpret_cast<const int*>(b + o_n1);
+  ds.yoff = reinterpret_cast<const int*>(b + o_yoff);
+  ds.nyhi = reinterpret_cast<const int*>(b + o_nyhi);
+  ds.upoff = reinterpret_cast<const int*>(b + o_upoff);
+  ds.dum = reinterpret_cast<const int*>(b + o_dum);
+  ds.pl_nb = reinterpret_cast<const int*>(b + o_plnb);
+  ds.pl_na = reinterpret_cast<const int*>(b + o_plna);
+  ds.pl_b = reinterpret_cast<const double*>(b + o_plb);
+  ds.pl_a = reinterpret_cast<const double*>(b + o_pla);
+  ds.bnd = reinterpret_cast<const double*>(b + o_bnd);
+  ds.yref = reinterpret_cast<const double*>(b + o_yref);
+  s->dtab = dp;
+  s->dev = dev;
+  return MPCT_OK;
+}
+
+static DevOpts make_opts(const mpct_opts* o) {
+  DevOpts d{};
+  d.open_loop = o ? o->open_loop : 0;
+  d.want_traj = o ? o->want_traj : 0;
+  d.max_qp_iter = o ? o->max_qp_iter : 0;
+  d.feas_tol = (o && o->feas_tol > 0) ? o->feas_tol : 1e-10;
+  return d;
+}
+
+static int check_args(mpct_scenario* s, int64_t C, int32_t nref, const int32_t* N2, const int32_t* Nu,
+                      const double* delta, const double* lambda, const double* r, const double* v) {
+  if (!s) return fail(MPCT_EINVAL, "null scenario");
+  if (C < 0 || nref < 1) return fail(MPCT_EINVAL, "C < 0 or nref < 1");
+  if (C * (int64_t)nref > 0x7fffffffLL) return fail(MPCT_ERANGE, "too many simulations in one call");
+  if (C > 0 && (!N2 || !Nu || !delta || !lambda || !r)) return fail(MPCT_EINVAL, "null input pointer");
+  if (s->nd > 0 && !v) return fail(MPCT_EINVAL, "v required when nd > 0");
+  return MPCT_OK;
+}
+
+extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                                          const double* delta, const double* lambda, int32_t nref,
+                                          const double* r, const double* v, const mpct_opts* opts,
+                                          mpct_result* out, void* stream) {
+  int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
+  if (rc) return rc;
+  if (!out) return fail(MPCT_EINVAL, "null result");
+  rc = ensure_device(s, opts ? opts->device : -1);
+  if (rc) return rc;
+  if (C == 0) return MPCT_OK;
+  DevOpts dop = make_opts(opts);
+  DevResult dr{out->J1, out->j21, out->j22, out->Jnu, out->status, out->qp_iters,
+                out->y, out->u, out->ys, out->uopt};
+  std::string err;
+  rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
+                          static_cast<hipStream_t>(stream), &err);
+  if (rc) return fail(rc, err);
+  return MPCT_OK;
+}
+
+extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                                   const double* delta, const double* lambda, int32_t nref, const double* r,
+                                   const double* v, const mpct_opts* opts, mpct_result* out) {
+  int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
+  if (rc) return rc;
+  if (!out) return fail(MPCT_EINVAL, "null result");
+  rc = ensure_device(s, opts ? opts->device : -1);
+  if (rc) return rc;
+  if (C == 0) return MPCT_OK;
+  const int my = s->my, nu = s->nu, nd = s->nd, nit = s->nit;
+  const int64_t S = C * nref;
+  const bool traj = opts && opts->want_traj;
+  const bool ol = opts && opts->open_loop;
+  // device scratch layout
+  size_t off = 0;
+  auto slot = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  size_t o_N2 = slot(C * 4), o_Nu = slot(C * 4), o_d = slot(C * my * 8), o_l = slot(C * nu * 8);
+  size_t o_r = slot((size_t)nref * my * nit * 8), o_v = slot((size_t)nref * nd * nit * 8);
+  size_t o_J1 = slot(S * my * 8), o_j21 = slot(S * my * 8), o_j22 = slot(S * my * 8), o_Jnu = slot(S * nu * 8);
+  size_t o_st = slot(S * 4), o_it = slot(S * 8);
+  size_t o_y = traj ? slot(S * my * nit * 8) : 0, o_u = traj ? slot(S * nu * nit * 8) : 0;
+  size_t o_ys = (traj && ol) ? slot(S * my * nit * 8) : 0, o_uo = (traj && ol) ? slot(S * nu * nit * 8) : 0;
+  if (off > s->dscratch_bytes) {
+    if (s->dscratch) (void)hipFree(s->dscratch);
+    s->dscratch = nullptr;
+    s->dscratch_bytes = 0;
+    if (hipMalloc(&s->dscratch, off) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(scratch) failed");
+    s->dscratch_bytes = off;
+  }
+  char* b = static_cast<char*>(s->dscratch);
+  auto h2d = [&](size_t o, const void* p, size_t bytes) {
+    return bytes == 0 || hipMemcpy(b + o, p, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!h2d(o_N2, N2, C * 4) || !h2d(o_Nu, Nu, C * 4) || !h2d(o_d, delta, C * my * 8) ||
+      !h2d(o_l, lambda, C * nu * 8) || !h2d(o_r, r, (size_t)nref * my * nit * 8) ||
+      (nd > 0 && !h2d(o_v, v, (size_t)nref * nd * nit * 8)))
+    return fail(MPCT_EDEVICE, "hipMemcpy(inputs) failed");
+  mpct_result dres{};
+  dres.J1 = reinterpret_cast<double*>(b + o_J1);
+  dres.j21 = reinterpret_cast<double*>(b + o_j21);
+  dres.j22 = reinterpret_cast<double*>(b + o_j22);
+  dres.Jnu = reinterpret_cast<double*>(b + o_Jnu);
+  dres.status = reinterpret_cast<int32_t*>(b + o_st);
+  dres.qp_iters = reinterpret_cast<int64_t*>(b + o_it);
+  if (traj) {
+    dres.y = reinterpret_cast<double*>(b + o_y);
+    dres.u = reinterpret_cast<double*>(b + o_u);
+    if (ol) {
+      dres.ys = reinterpret_cast<double*>(b + o_ys);
+      dres.uopt = reinterpret_cast<double*>(b + o_uo);
+    }
+  }
+  rc = mpct_eval_batch_device(s, C, reinterpret_cast<const int32_t*>(b + o_N2),
+                              reinterpret_cast<const int32_t*>(b + o_Nu),
+                              reinterpret_cast<const double*>(b + o_d),
+                              reinterpret_cast<const double*>(b + o_l), nref,
+                              reinterpret_cast<const double*>(b + o_r),
+                              nd > 0 ? reinterpret_cast<const double*>(b + o_v) : nullptr, opts, &dres,
+                              nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MPCT_EDEVICE, "kernel execution failed");
+  auto d2h = [&](void* dst, const void* src, size_t bytes) {
+    return !dst || bytes == 0 || hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+  };
+  bool ok = d2h(out->J1, dres.J1, S * my * 8) && d2h(out->j21, dres.j21, S * my * 8) &&
+            d2h(out->j22, dres.j22, S * my * 8) && d2h(out->Jnu, dres.Jnu, S * nu * 8) &&
+            d2h(out->status, dres.status, S * 4) && d2h(out->qp_iters, dres.qp_iters, S * 8);
+  if (traj) {
+    ok = ok && d2h(out->y, dres.y, S * my * nit * 8) && d2h(out->u, dres.u, S * nu * nit * 8);
+    if (ol) ok = ok && d2h(out->ys, dres.ys, S * my * nit * 8) && d2h(out->uopt, dres.uopt, S * nu * nit * 8);
+  }
+  if (!ok) return fail(MPCT_EDEVICE, "hipMemcpy(results) failed");
+  return MPCT_OK;
+}
+
+extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {
+  if (!s) return fail(MPCT_EINVAL, "null scenario");
+  DevScenario ds{};
+  ds.my = s->my;
+  ds.nu = s->nu;
+  ds.nin = s->nin;
+  ds.nx = s->nx;
+  ds.ne = s->ne;
+  ds.tlen = s->tlen;
+  return lds_bytes_for(ds, N2, Nu);
+}

@@ -1,0 +1,233 @@
+"""Restated DTC-GPC primitives (reference ``DTC-GPC/*.m``) — oracle, test infrastructure only.
+
+Indexing: Python lists of lists stand in for MATLAB cells ``{i,j}``; all horizons/rows are
+1-based in the docstrings (as in the .m files) and 0-based in code.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .matlab import DTF, conv, mround, poly, roots, step_dtf
+
+
+# ---------------------------------------------------------------------------------------------
+def descomp_mpc(P):
+    """descompMPC.m:19-43.  ``P`` is an my x nin matrix of DTF (tfdata 'v' form).
+
+    Returns (B, A, d): cells of numerator / denominator rows and the delay matrix, after the
+    two adjustments of descompMPC.m:35-41:
+      * if B{i,j}(1) ~= 0: d(i,j) = d(i,j)-1 and B{i,j} = [0 B{i,j}]   (keep u(k-1) causal)
+      * if dcgain(P(i,j)) == 0: d(i,j) = max(d(i,:))   (zero entry takes the row's max delay)
+    """
+    my = len(P)
+    nin = len(P[0])
+    B = [[None] * nin for _ in range(my)]
+    A = [[None] * nin for _ in range(my)]
+    d = np.zeros((my, nin), dtype=int)
+    for i in range(my):
+        for j in range(nin):
+            B[i][j] = np.array(P[i][j].num, dtype=float)
+            A[i][j] = np.array(P[i][j].den, dtype=float)
+            d[i, j] = P[i][j].iodelay
+    for i in range(my):
+        for j in range(nin):
+            if B[i][j][0] != 0:  # Q = inf default -> condition u < Q(1) always true
+                d[i, j] -= 1
+                B[i][j] = np.concatenate([[0.0], B[i][j]])
+            if P[i][j].dcgain() == 0:
+                d[i, j] = d[i, :].max()
+    return B, A, d
+
+
+# ---------------------------------------------------------------------------------------------
+def ba_mimo(Bn, An, round_roots: bool = True):
+    """BA_MIMO.m:20-71.  Least-common-multiple denominator per output row and the matching
+    numerators.
+
+    round_roots=True is the reference verbatim: LCM poles are ``unique(round(roots(prod),4))``
+    (BA_MIMO.m:141-143) and B{i,j} = Bn{i,j} * poly(LCM roots not in round(roots(An{i,j}),4))
+    (BA_MIMO.m:151-163), including its index-skipping removal loop.  This perturbs the model by
+    ~1e-5 (a deliberate model change in the reference).
+
+    round_roots=False is the exact-model variant used for toolbox-equivalent semantics
+    (SURVEY §7 "two modes"): the LCM is the product of the DISTINCT denominator polynomials of
+    the row (duplicates detected by coefficient equality), so the CARIMA model equals the plant
+    up to rounding.  Returns (B, A, na, nb) with A a list (A{i,i}).
+    """
+    p = len(An)
+    m = len(An[0])
+    Bn = [[np.array(Bn[i][j], dtype=float) for j in range(m)] for i in range(p)]
+    for i in range(p):
+        for j in range(m):
+            if Bn[i][j][0] == 0:  # BA_MIMO.m:125-127 strip ONE leading zero
+                Bn[i][j] = Bn[i][j][1:]
+    A = [None] * p
+    B = [[None] * m for _ in range(p)]
+    if round_roots:
+        for i in range(p):
+            aux = An[i][0]
+            for j in range(1, m):
+                aux = conv(aux, An[i][j])
+            A[i] = aux
+            if p != 1:
+                au1 = mround(roots(aux), 4)
+                pol = np.unique(au1)
+                A[i] = np.real(poly(pol))
+        for i in range(p):
+            for j in range(m):
+                aux = Bn[i][j]
+                rA = list(mround(roots(A[i]), 4))
+                rAn = list(mround(roots(An[i][j]), 4))
+                kk = 0
+                while kk < len(rA):
+                    for jj in range(len(rAn)):
+                        # MATLAB: if rA(kk)==rAn(jj), rA = rA(rA ~= rA(kk)) — index may now be
+                        # out of range for the next jj (MATLAB would error); keep the same order.
+                        if rA[kk] == rAn[jj]:
+                            v = rA[kk]
+                            rA = [x for x in rA if x != v]
+                            if kk >= len(rA):
+                                break
+                    kk += 1
+                pA = np.real(poly(np.array(rA))) if rA else np.ones(1)
+                B[i][j] = conv(aux, pA)
+    else:
+        for i in range(p):
+            uniq = []
+            for j in range(m):
+                dj = np.asarray(An[i][j], dtype=float)
+                if not any(len(dj) == len(u) and np.array_equal(dj, u) for u in uniq):
+                    uniq.append(dj)
+            A[i] = np.ones(1)
+            for u in uniq:
+                A[i] = conv(A[i], u)
+            for j in range(m):
+                aux = Bn[i][j]
+                dj = np.asarray(An[i][j], dtype=float)
+                for u in uniq:
+                    if not (len(dj) == len(u) and np.array_equal(dj, u)):
+                        aux = conv(aux, u)
+                B[i][j] = aux
+    na = np.array([len(A[i]) - 1 for i in range(p)])
+    nb = np.array([[len(B[i][j]) - 1 for j in range(m)] for i in range(p)])
+    return B, A, na, nb
+
+
+# ---------------------------------------------------------------------------------------------
+def diophantine(A, N: int, d: int):
+    """diophantine.m:23-79 (Normey-Rico & Camacho).  A~ = conv(A,[1 -1]); F rows for the window
+    N1 = d+1 .. N2 = d+N; E rows N1..N2 (each a length-N2 row, E_j left-aligned)."""
+    AD = conv(A, [1.0, -1.0])
+    nAD = len(AD)
+    N1 = d + 1
+    N2 = d + N
+    f = np.zeros((N2 + 1, nAD - 1))
+    f[0, 0] = 1.0
+    for j in range(N2):
+        for i in range(nAD - 2):
+            f[j + 1, i] = f[j, i + 1] - f[j, 0] * AD[i + 1]
+        f[j + 1, nAD - 2] = -f[j, 0] * AD[nAD - 1]
+    F = f[N1: N2 + 1, :]
+    E = np.zeros((N2, N2))
+    e = [1.0]
+    E[0, 0] = 1.0
+    for i in range(2, N2 + 1):
+        e.append(f[i - 1, 0])
+        E[i - 1, :i] = e
+    E = E[N1 - 1: N2, :]
+    return E, F
+
+
+def diophantine_mimo(A, N, dmin):
+    """diophantineMIMO.m:15-21 — per output on A{i,i}.  Returns (E, En, F) lists."""
+    E, En, F = [], [], []
+    for i in range(len(A)):
+        En1, Fn = diophantine(A[i], int(N[i]), int(dmin[i]))
+        E.append(En1[-1, :])
+        F.append(Fn)
+        En.append(En1)
+    return E, En, F
+
+
+# ---------------------------------------------------------------------------------------------
+def mat_g(P, N, Nu, d):
+    """MatG.m:38-74.  Dynamic matrix from step responses:
+    G{i,j}(k:end, k) = g(dmin(i)+2 : dmin(i)+N(i)-k+2), g = step(P(i,j), (N(i)+dmin(i))*Ts).
+
+    Row r (0-based) of block i therefore predicts y_i(t + dmin(i) + 1 + r); column c is
+    Delta u_j(t + c).  Passing d == 0 gives the toolbox window t+1..t+N.  Returns (MG, MGc)."""
+    s = len(P)
+    e = len(P[0]) if s else 0
+    d = np.atleast_2d(np.asarray(d))
+    dmin = d.ravel() if e == 1 else d.min(axis=1)
+    H = [[None] * e for _ in range(s)]
+    for i in range(s):
+        for j in range(e):
+            g = step_dtf(P[i][j], int(N[i] + dmin[i]) + 1)
+            G = np.zeros((int(N[i]), int(Nu[j])))
+            for k in range(1, int(Nu[j]) + 1):
+                lo = int(dmin[i]) + 2
+                hi = int(dmin[i]) + int(N[i]) - k + 2
+                G[k - 1:, k - 1] = g[lo - 1: hi]
+            H[i][j] = G
+    MG = np.block(H)
+    return MG, H
+
+
+# ---------------------------------------------------------------------------------------------
+def delta_u_free(B, En, N, dp):
+    """deltaUFree.m:13-62.  uG{m,n}(i,:) = last cp coefficients of conv(En{m}(i,:), B{m,n})
+    after removing ALL zero coefficients (deltaUFree.m:302-308: the loop keeps aux(j) ~= 0 for
+    every j, not only trailing ones), cp = dp(m,n) + length(B{m,n}) - 1, left-padded with zeros
+    when shorter.  Column order: Delta u(t-1), Delta u(t-2), ..., Delta u(t-cp)."""
+    ny = len(B)
+    nu = len(B[0])
+    uG = [[None] * nu for _ in range(ny)]
+    for m in range(ny):
+        for n in range(nu):
+            cp = int(dp[m][n]) + len(B[m][n]) - 1
+            if cp < 1:
+                cp = 1
+            uG1 = np.zeros((int(N[m]), cp))
+            for i in range(int(N[m])):
+                aux = conv(En[m][i, :], B[m][n])
+                BE = [a for a in aux if a != 0]
+                lBE = len(BE)
+                if lBE < cp:
+                    uG1[i, :] = np.concatenate([np.zeros(cp - lBE), BE])
+                else:
+                    uG1[i, :] = BE[lBE - cp:]
+            uG[m][n] = uG1
+    return uG
+
+
+def cell2mat2(Bc):
+    """cell2mat2.m:25-58 — left-aligned block assembly; block column width = max rows' widths,
+    block row height = max columns' heights."""
+    m = len(Bc)
+    n = len(Bc[0])
+    f1 = np.array([[Bc[i][j].shape[0] for j in range(n)] for i in range(m)])
+    c1 = np.array([[Bc[i][j].shape[1] for j in range(n)] for i in range(m)])
+    c1m = np.concatenate([[0], c1.max(axis=0)])
+    f1m = np.concatenate([[0], f1.max(axis=1)])
+    n1 = max(c1[i].sum() for i in range(m))
+    m1 = f1.max(axis=1).sum()
+    A = np.zeros((m1, max(n1, c1m.sum())))
+    for i in range(m):
+        for j in range(n):
+            r0 = f1m[: i + 1].sum()
+            c0 = c1m[: j + 1].sum()
+            A[r0: r0 + f1[i, j], c0: c0 + c1[i, j]] = Bc[i][j]
+    return A[:, : c1m.sum()]
+
+
+def blkdiag(*mats):
+    rows = sum(a.shape[0] for a in mats)
+    cols = sum(a.shape[1] for a in mats)
+    out = np.zeros((rows, cols))
+    r = c = 0
+    for a in mats:
+        out[r: r + a.shape[0], c: c + a.shape[1]] = a
+        r += a.shape[0]
+        c += a.shape[1]
+    return out

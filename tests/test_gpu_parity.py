@@ -1,0 +1,168 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle on the same inputs.
+
+Tolerance (BASELINE.json north_star): <= 1e-6 relative on du / closed-loop cost; we also hold
+trajectories to 1e-7 of their peak magnitude (TRAJ_RTOL) and require an identical
+candidate ranking (cost ascending, candidate-index tiebreak).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TRAJ_RTOL = 1e-7   # max |a-b| / max |b| per trajectory (BASELINE: 1e-6 relative on du, cost)
+COST_RTOL = 1e-6
+
+
+def _trel(a, b):
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def env(built, has_gpu):
+    if not has_gpu:
+        pytest.skip("no GPU")
+    from mpct.scenarios import shell3x3
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3
+
+    sc, r, yref = shell3x3(n2_max=30, nu_max=6)
+    osc, orr, oyref, fx = o_shell3x3()
+    assert np.array_equal(r, orr) and np.allclose(yref, oyref, rtol=0, atol=1e-15)
+    cp = CPort(osc, 30, 500, oyref)
+    return dict(sc=sc, r=r, yref=yref, osc=osc, cp=cp, fx=fx)
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-12)))
+
+
+def test_trajectories_match_oracle(env):
+    from mpct.engine import eval_batch
+    from mpct.scenarios import candidate_grid
+
+    N2, Nu, d, l = candidate_grid(6)
+    res = eval_batch(env["sc"], N2, Nu, d, l, env["r"][None], open_loop=True, want_traj=True)
+    ref = env["cp"].eval(N2, Nu, d, l, env["r"][None], open_loop=True, want_traj=True)
+    assert np.all(res.status == 0) and np.all(ref["status"] == 0)
+    for k in ("y", "u", "ys", "uopt"):
+        e = _trel(getattr(res, k), ref[k])
+        print("traj", k, e)
+        assert e < TRAJ_RTOL, (k, e)
+    assert _rel(res.J1, ref["J1"]) < COST_RTOL
+    assert _rel(res.j22, ref["j22"]) < COST_RTOL
+
+
+def test_numpy_oracle_fixture_point(env):
+    """The committed tuned point (Shell3x3_Tuning_25Jul2023: N=24, Nu=[6 2 2] -> max 6) through
+    the drop-in closedloop_toolbox vs the numpy oracle (primal active-set QP)."""
+    from mpct.engine import closedloop_toolbox
+    from oracle.toolbox_gpc import closedloop_toolbox as o_cl
+
+    fx = env["fx"]
+    y, u, t, ys, uopt = closedloop_toolbox(env["sc"], env["r"], None, fx["N"], fx["Nu"], fx["delta"],
+                                           fx["lambda"], 500)
+    ref = o_cl(env["osc"], env["r"], None, 24, 6, fx["delta"], fx["lambda"], 500, open_loop=True)
+    assert _trel(y, ref.y) < TRAJ_RTOL, _trel(y, ref.y)
+    assert _trel(u, ref.u) < TRAJ_RTOL, _trel(u, ref.u)
+    assert _trel(ys, ref.ys) < TRAJ_RTOL, _trel(ys, ref.ys)
+    assert _trel(uopt, ref.uopt) < TRAJ_RTOL, _trel(uopt, ref.uopt)
+    assert t[1] - t[0] == 4.0
+
+
+def test_costs_and_ranking(env):
+    from mpct.engine import eval_batch
+    from mpct.objectives import rank
+    from mpct.scenarios import candidate_grid
+
+    N2, Nu, d, l = candidate_grid(96)
+    res = eval_batch(env["sc"], N2, Nu, d, l, env["r"][None])
+    ref = env["cp"].eval(N2, Nu, d, l, env["r"][None])
+    assert np.all(res.status == 0)
+    assert _rel(res.J1, ref["J1"]) < COST_RTOL
+    w = np.array([0.05, 0.40, 0.55])  # Shell3x3.m:161 Pareto weights
+    assert np.array_equal(rank(res.J1 @ w), rank(ref["J1"] @ w))
+    assert np.array_equal(rank(res.J1.sum(1)), rank(ref["J1"].sum(1)))
+
+
+def test_vns_objective(env):
+    from mpct.objectives import vns_objective
+    from mpct.scenarios import candidate_grid, vns_step_refs
+
+    N2, Nu, d, l = candidate_grid(5)
+    N2 = np.array([30, 24, 16, 12, 30], dtype=np.int32)
+    Nu = np.array([5, 6, 3, 2, 1], dtype=np.int32)
+    F, j21, j22, jnu, res = vns_objective(env["sc"], N2, Nu, d, l)
+    refs = vns_step_refs(3, 500)
+    ref = env["cp"].eval(N2, Nu, d, l, refs, open_loop=True)
+    idx = np.arange(3)
+    rj21 = ref["j21"].reshape(5, 3, 3)[:, idx, idx]
+    rj22 = ref["j22"].reshape(5, 3, 3)[:, idx, idx]
+    assert np.all(res.status == 0)
+    assert _rel(j21, rj21) < COST_RTOL
+    assert _rel(j22, rj22) < COST_RTOL
+    # Jnu divides by |diff(uopt)| (VNS2.m:185): compare where the oracle's moves are not tiny
+    rjnu = ref["Jnu"].reshape(5, 3, 3)[:, idx, idx]
+    ok = rjnu < 1e6
+    assert _rel(jnu[ok], rjnu[ok]) < 1e-5
+
+
+def test_gpc_window_unsquared_and_rounded(env, built):
+    """MatG/DTC window (t+dmin+1..), DTC_GPC_WW.m weighting (unsquared) and BA_MIMO's rounded
+    LCM, each against the oracle built the same way."""
+    from mpct.engine import eval_batch
+    from mpct.scenarios import candidate_grid, shell3x3
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3
+
+    N2, Nu, d, l = candidate_grid(8, N2=20, Nu=4)
+    for kw, okw in [(dict(window="gpc"), dict(window="gpc")),
+                    (dict(weights_squared=False), dict(weights_squared=False)),
+                    (dict(exact_carima=False), dict(round_roots=True))]:
+        sc, r, yref = shell3x3(n2_max=20, nu_max=4, **kw)
+        osc, orr, oyref, _ = o_shell3x3(**okw)
+        cp = CPort(osc, 20, 500, oyref)
+        res = eval_batch(sc, N2, Nu, d, l, r[None], want_traj=True)
+        ref = cp.eval(N2, Nu, d, l, orr[None], want_traj=True)
+        assert np.all(res.status == 0), kw
+        assert _trel(res.y, ref["y"]) < TRAJ_RTOL, (kw, _trel(res.y, ref["y"]))
+        assert _rel(res.J1, ref["J1"]) < COST_RTOL, kw
+
+
+def test_full_grid_properties(env):
+    """Full metric batch (4096 candidates): clean status, finite costs, bitwise determinism and
+    independence from batch order / composition."""
+    from mpct.engine import eval_batch
+    from mpct.scenarios import candidate_grid
+
+    N2, Nu, d, l = candidate_grid(4096)
+    a = eval_batch(env["sc"], N2, Nu, d, l, env["r"][None])
+    b = eval_batch(env["sc"], N2, Nu, d, l, env["r"][None])
+    assert np.all(a.status == 0)
+    assert np.all(np.isfinite(a.J1))
+    assert np.array_equal(a.J1, b.J1)
+    perm = np.random.default_rng(1).permutation(4096)
+    c = eval_batch(env["sc"], N2[perm], Nu[perm], d[perm], l[perm], env["r"][None])
+    assert np.array_equal(c.J1, a.J1[perm])
+    # a sample of the batch against the C port
+    idx = np.arange(0, 4096, 97)
+    ref = env["cp"].eval(N2[idx], Nu[idx], d[idx], l[idx], env["r"][None])
+    assert _rel(a.J1[idx], ref["J1"]) < COST_RTOL
+
+
+def test_status_edges(env):
+    from mpct.engine import eval_batch
+
+    sc = env["sc"]
+    N2 = np.array([0, 30, 4, 31], dtype=np.int32)
+    Nu = np.array([5, 5, 6, 5], dtype=np.int32)
+    d = np.full((4, 3), 0.1)
+    l = np.full((4, 3), 0.01)
+    res = eval_batch(sc, N2, Nu, d, l, env["r"][None])
+    assert res.status[0] == 8            # skipped sentinel
+    assert res.status[1] == 0
+    assert res.status[2] == 16           # Nu > N2
+    assert res.status[3] == 16           # N2 > n2_max
+    assert np.all(np.isnan(res.J1[[0, 2, 3]]))
+    empty = eval_batch(sc, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 3)),
+                       np.zeros((0, 3)), env["r"][None])
+    assert empty.J1.shape == (0, 3)
