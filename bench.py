@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: closed-loop GPC simulations/s over the Shell 3x3 tuning grid (BASELINE.json metric).
+
+One step = score one batch of 4096 (N2=30, Nu=5, delta, lambda) candidates per GPU: a 500-step
+constrained closed loop + its GAM cost J1 per candidate (GAM_fun.m:81-111 per candidate), then
+one RCCL all-gather of the per-candidate costs and an identical stable ranking on every rank
+(SURVEY §8e).  Inputs are resident in HBM before the timed region.  Weak scaling: every rank
+scores its own contiguous 4096-candidate shard of a (4096 x world)-candidate grid.
+
+Launch:  python bench.py [--gpus 1 --steps K --warmup W]
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "model-predictive-control-tuning_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) dense peak, AMD spec; see DESIGN.md
+
+
+def algorithmic_flops_per_sim(sc, N2, Nu, iters_per_step):
+    """SURVEY §8(d) per-simulation flop count, evaluated on this scenario's tables:
+    setup P*M*(M+1) + M^3/3; per step: plant 5*my*(nu+nd) + free response
+    2*N2*(sum(na+1) + sum_ij cp_ij) + gradient 2*P*(M+1) + solve 2*M^2 + active set
+    2*(2M*M + M^2)*I_as + cost 4*my."""
+    my, nu, nin = sc.my, sc.nu, sc.nin
+    M, P = nu * Nu, my * N2
+    cp = sc.dp[:, :nu] + sc.nb[:, :nu]
+    setup = P * M * (M + 1) + M ** 3 / 3.0
+    per_step = (5 * my * nin + 2 * N2 * (int(np.sum(sc.na + 1)) + int(np.sum(np.maximum(cp, 1))))
+                + 2 * P * (M + 1) + 2 * M * M + 2 * (2 * M * M + M * M) * iters_per_step + 4 * my)
+    return setup + sc.nit * per_step
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--candidates", type=int, default=4096, help="candidates per GPU per step")
+    ap.add_argument("--n2", type=int, default=30)
+    ap.add_argument("--nu", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+
+        tdist.init_process_group("nccl", device_id=dev)
+
+    from mpct.engine import eval_batch, eval_batch_device
+    from mpct.scenarios import candidate_grid, shell3x3
+
+    sc, r, yref = shell3x3(n2_max=args.n2, nu_max=args.nu)
+    Cg = args.candidates * world
+    N2, Nu, d, l = candidate_grid(Cg, N2=args.n2, Nu=args.nu)
+    lo, hi = rank * args.candidates, (rank + 1) * args.candidates
+    # inputs resident in HBM before the timed region
+    tN2 = torch.from_numpy(N2[lo:hi].copy()).to(dev)
+    tNu = torch.from_numpy(Nu[lo:hi].copy()).to(dev)
+    td = torch.from_numpy(d[lo:hi].copy()).to(dev)
+    tl = torch.from_numpy(l[lo:hi].copy()).to(dev)
+    tr = torch.from_numpy(r[None].copy()).to(dev)
+    C = hi - lo
+    out = dict(J1=torch.empty((C, sc.my), dtype=torch.float64, device=dev),
+               j22=torch.empty((C, sc.my), dtype=torch.float64, device=dev),
+               status=torch.empty(C, dtype=torch.int32, device=dev),
+               qp_iters=torch.empty(C, dtype=torch.int64, device=dev))
+    gathered = torch.empty((world * C, sc.my), dtype=torch.float64, device=dev)
+    w = torch.tensor([0.05, 0.40, 0.55], dtype=torch.float64, device=dev)  # Shell3x3.m:161
+    stream = torch.cuda.current_stream(dev)
+    kev = []
+
+    def step(record):
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        eval_batch_device(sc, tN2, tNu, td, tl, tr, out, device=local, stream=stream)
+        if record:
+            e1.record(stream)
+            kev.append((e0, e1))
+        if dist:
+            tdist.all_gather_into_tensor(gathered, out["J1"])
+            costs = gathered @ w
+        else:
+            costs = out["J1"] @ w
+        return torch.argsort(costs, stable=True)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        order = step(True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(te, op=tdist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))  # ms per kernel launch
+    status = out["status"].cpu().numpy()
+    iters = out["qp_iters"].cpu().numpy()
+    nbad = int(np.count_nonzero(status))
+    I_as = float(iters.mean() / sc.nit)
+    sims = world * C * args.steps
+    value = sims / elapsed
+    fl = algorithmic_flops_per_sim(sc, args.n2, args.nu, I_as) * C
+    achieved = fl / (kms * 1e-3) / 1e12
+
+    if rank != 0:
+        if dist:
+            tdist.destroy_process_group()
+        return
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pj = json.load(f)
+            if pj.get("candidates") == C and pj.get("n2") == args.n2 and pj.get("nu") == args.nu:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        # oracle/cgpc.c (C restatement of the same closed loop), timed on this host's cores
+        from oracle.cport import CPort
+        from oracle.scenarios import shell3x3 as o_shell3x3
+
+        osc, orr, oyref, _ = o_shell3x3()
+        cp = CPort(osc, args.n2, sc.nit, oyref)
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        threads = max(1, min(threads, 64))
+        ncpu = C
+        t1 = time.perf_counter()
+        ref = cp.eval(N2[:ncpu], Nu[:ncpu], d[:ncpu], l[:ncpu], orr[None], threads=threads)
+        tc = time.perf_counter() - t1
+        gpuJ = out["J1"].cpu().numpy()[:ncpu]
+        rel = float(np.max(np.abs(gpuJ - ref["J1"]) / np.maximum(np.abs(ref["J1"]), 1e-12)))
+        cpu = {"value": ncpu / tc, "unit": "sims/s", "cores": threads, "kind": "port",
+               "sample": "oracle/cgpc.c on the same %d-candidate Shell 3x3 batch (N2=%d, Nu=%d, nit=500), "
+                         "1 pass, %d OpenMP threads, %.1f s wall; max rel |J1_gpu - J1_cpu| = %.1e"
+                         % (ncpu, args.n2, args.nu, threads, tc, rel)}
+
+    line = {
+        "metric": "closed-loop GPC sims/sec (Shell 3x3, N2=30 Nu=5) over tuning grid",
+        "value": value,
+        "unit": "sims/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic candidate grid (numpy default_rng(20250307)) on the reference's Shell 3x3 "
+                "scenario (Shell3x3.m caso 2, L/R from Shell3x3_Tuning_25Jul2023_12_06.mat)",
+        "config": {"workload": "Shell3x3 GAM scoring: %d candidates/GPU x nit=500 closed loop + J1 + "
+                               "RCCL all-gather + ranking" % C,
+                   "candidates_per_gpu": C, "N2": args.n2, "Nu": args.nu, "nit": sc.nit,
+                   "parallelism": "dp%d" % world},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "gpc_closed_loop_kernel", "kernel_ms": kms,
+                     "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as},
+        "cpu_baseline": cpu,
+        "status_nonzero": nbad,
+        "top_candidate": int(order[0].item()),
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -115,22 +115,32 @@ __device__ __forceinline__ void lane_slacks(const double* __restrict__ sxc, int 
   }
 }
 
-// Goldfarb-Idnani dual active-set QP in Schur-complement form, starting from the unconstrained
-// minimiser already in sxc[0..M).  min 1/2 x'Hx + g'x, H^-1 in LDS.  Returns iterations; sets
-// *st bits.  All lanes call it (wave-uniform control flow).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Goldfarb-Idnani dual active-set QP, numerically stable form:
+// with H = R'R (R from the QR of W = [Q^1/2 G; Lambda^1/2]) and B = R^-T N_W for the active
+// normals, each iteration recomputes the Householder QR of [B | b_p] (lanes = columns):
+//   [c; tail] = Qb' b_p,  r = Rb^-1 c,  e = Qb [0; tail],  z = R^-1 e,  beta = n_p'z = |tail|^2.
+// Starts from the unconstrained minimiser in sxc[0..M).  R^-1 (upper, row-major) is in
+// lds[L.hinv].  Returns inner iterations; sets *st bits.  Wave-uniform control flow.
+template <int MAXM>
 __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, int nu,
                      const double* bnd, double tol, int maxit, int* st) {
   const int lane = threadIdx.x;
-  double* sH = lds + L.hinv;
+  const double* sRi = lds + L.hinv;
   double* sxc = lds + L.xc;
-  double* sv_ = lds + L.v;
-  double* sz = lds + L.z;
+  double* sbp = lds + L.v;
+  double* se = lds + L.z;
   double* sr = lds + L.r;
   double* su = lds + L.u;
-  double* ssv = lds + L.sv;
-  double* sY = lds + L.Y;
-  double* sS = lds + L.sinv;
-  double* sT = lds + L.tmp;
+  double* sc_ = lds + L.sv;
+  double* sB = lds + L.Y;     // active b_w columns [w][m]
+  double* sRb = lds + L.sinv; // Rb columns [w][k]
+  double* sV = lds + L.tmp;   // reflectors [j][k]
   double* suprev = lds + L.uprev;
   int* sW = reinterpret_cast<int*>(lds + L.wid);
   unsigned act = 0;  // active bits of this lane's 4 constraints
@@ -152,62 +162,118 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
     }
     wave_argmin(best, bid);
     if (!(best < -tol)) break;
-    if (it >= maxit) {
+    if (it >= maxit || q >= M) {
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
     const int p = bid;
     const CInfo cp = cinfo(p, Nu);
+    // b_p = R^-T n_p:  b_p[m] = sg * sum_{j in S_p} Rinv[j][m]
+    double bpm = 0.0;
+    if (lane < M) {
+      for (int j = cp.j0; j <= cp.j1; ++j) bpm += sRi[j * M + lane];
+      bpm *= cp.sg;
+      sbp[lane] = bpm;
+    }
+    const double bpn = wave_sum(bpm * bpm);
     double sp = best;  // current slack of p
     double up = 0.0;   // its multiplier
+    __syncthreads();
     for (;;) {
       ++it;
-      // v = H^-1 n_p  (H^-1 symmetric: read row j, lanes contiguous)
-      double vm = 0.0;
-      if (lane < M) {
-        for (int j = cp.j0; j <= cp.j1; ++j) vm += sH[j * M + lane];
-        vm *= cp.sg;
-        sv_[lane] = vm;
+      // ---- Householder QR of [B | b_p], lane w holds column w (w < q: b_w, w == q: b_p)
+      double col[MAXM];
+      const double* src = lane < q ? sB + lane * M : sbp;
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k) col[k] = (lane <= q && k < M) ? src[k] : 0.0;
+      for (int j = 0; j < q; ++j) {
+        if (lane == j) {
+          double nrm = 0.0, cj = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXM; ++k)
+            if (k >= j && k < M) nrm += col[k] * col[k];
+#pragma unroll
+          for (int k = 0; k < MAXM; ++k)
+            if (k == j) cj = col[k];
+          nrm = sqrt(nrm);
+          const double alpha = cj > 0.0 ? -nrm : nrm;
+          double vn = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXM; ++k) {
+            if (k < M) {
+              double v = k < j ? 0.0 : (k == j ? col[k] - alpha : col[k]);
+              sV[j * M + k] = v;
+              vn += v * v;
+              col[k] = k < j ? col[k] : (k == j ? alpha : 0.0);
+            }
+          }
+          sc_[j] = vn;  // |v_j|^2 (sc_ reused: c is read from the b_p lane later)
+        }
+        __syncthreads();
+        if (lane > j && lane <= q) {
+          const double vn = sc_[j];
+          if (vn != 0.0) {
+            double dt = 0.0;
+#pragma unroll
+            for (int k = 0; k < MAXM; ++k)
+              if (k >= j && k < M) dt += sV[j * M + k] * col[k];
+            const double f = 2.0 * dt / vn;
+#pragma unroll
+            for (int k = 0; k < MAXM; ++k)
+              if (k >= j && k < M) col[k] -= f * sV[j * M + k];
+          }
+        }
       }
-      __syncthreads();
+      // Rb columns to LDS; lane q: c (k < q) and tail (k >= q)
       if (lane < q) {
-        CInfo cw = cinfo(sW[lane], Nu);
-        double a = 0.0;
-        for (int j = cw.j0; j <= cw.j1; ++j) a += sv_[j];
-        ssv[lane] = cw.sg * a;
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+          if (k < M) sRb[lane * M + k] = col[k];
       }
-      __syncthreads();
-      if (lane < q) {
-        double a = 0.0;
-        for (int w = 0; w < q; ++w) a += sS[lane * M + w] * ssv[w];
-        sr[lane] = a;
+      double beta_part = 0.0;
+      if (lane == q) {
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+          if (k < M) {
+            se[k] = k < q ? 0.0 : col[k];
+            if (k >= q) beta_part += col[k] * col[k];
+            if (k < q) sr[k] = col[k];  // c, solved in place below
+          }
       }
+      const double beta = wave_sum(beta_part);
       __syncthreads();
-      double zm = vm;
+      // e = H_0 ... H_{q-1} [0; tail]   (lanes = components)
+      double ek = lane < M ? se[lane] : 0.0;
+      for (int j = q - 1; j >= 0; --j) {
+        const double vn = sc_[j];
+        const double vk = (lane >= j && lane < M) ? sV[j * M + lane] : 0.0;
+        const double dt = wave_sum(vk * ek);
+        if (vn != 0.0) ek -= (2.0 * dt / vn) * vk;
+      }
+      // r = Rb^-1 c  (column-oriented back substitution, lane k holds c_k)
+      double ck = lane < q ? sr[lane] : 0.0;
+      double rk = 0.0;
+      for (int w = q - 1; w >= 0; --w) {
+        const double rw = __shfl(ck, w, 64) / sRb[w * M + w];
+        if (lane == w) rk = rw;
+        if (lane < w) ck -= sRb[w * M + lane] * rw;
+      }
+      if (lane < M) se[lane] = ek;
+      __syncthreads();
+      // z = R^-1 e
+      double zm = 0.0;
       if (lane < M) {
-        for (int w = 0; w < q; ++w) zm -= sY[w * M + lane] * sr[w];
-        sz[lane] = zm;
+        for (int k = lane; k < M; ++k) zm += sRi[lane * M + k] * se[k];
       }
-      __syncthreads();
-      double beta = 0.0, cpp = 0.0;
-      for (int j = cp.j0; j <= cp.j1; ++j) {
-        beta += sz[j];
-        cpp += sv_[j];
-      }
-      beta *= cp.sg;
-      cpp *= cp.sg;
       // dual step length t1 over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
-      if (lane < q) {
-        double rw = sr[lane];
-        if (rw > 0.0) {
-          t1 = su[lane] / rw;
-          kdrop = lane;
-        }
+      if (lane < q && rk > 0.0) {
+        t1 = su[lane] / rk;
+        kdrop = lane;
       }
       wave_argmin(t1, kdrop);
-      double t2 = (beta > 1e-14 * cpp) ? -sp / beta : INFINITY;
+      const double t2 = (beta > 1e-14 * bpn) ? -sp / beta : INFINITY;
       if (t1 == INFINITY && t2 == INFINITY) {
         *st |= MPCT_ST_QP_INFEAS_;
         if (lane < M) sxc[lane] = xm;
@@ -220,32 +286,12 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
         xm += t * zm;
         sxc[lane] = xm;
       }
-      if (lane < q) su[lane] -= t * sr[lane];
+      if (lane < q) su[lane] -= t * rk;
       up += t;
       sp += t * beta;
       __syncthreads();
       if (full) {
-        // add p: Y(:,q) = v, Sinv block update, multiplier, id
-        if (lane < M) sY[q * M + lane] = vm;
-        const double ib = 1.0 / beta;
-        for (int e = lane; e < (q + 1) * (q + 1); e += kWave) {
-          int a = e / (q + 1), b = e - a * (q + 1);
-          double val;
-          if (a < q && b < q)
-            val = sS[a * M + b] + sr[a] * sr[b] * ib;
-          else if (a < q)
-            val = -sr[a] * ib;
-          else if (b < q)
-            val = -sr[b] * ib;
-          else
-            val = ib;
-          sT[a * M + b] = val;
-        }
-        __syncthreads();
-        for (int e = lane; e < (q + 1) * (q + 1); e += kWave) {
-          int a = e / (q + 1), b = e - a * (q + 1);
-          sS[a * M + b] = sT[a * M + b];
-        }
+        if (lane < M) sB[q * M + lane] = sbp[lane];
         if (lane == 0) {
           su[q] = up;
           sW[q] = p;
@@ -255,28 +301,17 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
         __syncthreads();
         break;
       }
-      // drop kdrop: Schur downdate of Sinv, move slot q-1 into kdrop
+      // drop kdrop, keeping the order of the remaining columns
       {
         const int k = kdrop;
         const int idk = sW[k];
         if (lane == (idk >> 2)) act &= ~(1u << (idk & 3));
-        const double ikk = 1.0 / sS[k * M + k];
-        for (int e = lane; e < q * q; e += kWave) {
-          int a = e / q, b = e - a * q;
-          if (a == k || b == k) continue;
-          int na_ = (a == q - 1) ? k : a, nb_ = (b == q - 1) ? k : b;
-          sT[na_ * M + nb_] = sS[a * M + b] - sS[a * M + k] * sS[k * M + b] * ikk;
-        }
         __syncthreads();
-        for (int e = lane; e < (q - 1) * (q - 1); e += kWave) {
-          int a = e / (q - 1), b = e - a * (q - 1);
-          sS[a * M + b] = sT[a * M + b];
-        }
-        if (k != q - 1) {
-          if (lane < M) sY[k * M + lane] = sY[(q - 1) * M + lane];
+        for (int w = k; w < q - 1; ++w) {
+          if (lane < M) sB[w * M + lane] = sB[(w + 1) * M + lane];
           if (lane == 0) {
-            su[k] = su[q - 1];
-            sW[k] = sW[q - 1];
+            su[w] = su[w + 1];
+            sW[w] = sW[w + 1];
           }
         }
         --q;
@@ -351,140 +386,105 @@ __global__ void __launch_bounds__(64)
   const double* dl = deltav + c * my;
   const double* lm = lambdav + c * nu;
 
-  // Columns of [G | Phi_dev] (ncol = M + nx), one per lane, in chunks of 64:
-  //   acc[a] = sum_i w_i sum_{r<N2} G(i,r,a) * col_l(i,r)   ->  H = G'QG (+Lambda), K = G'Q Phi
-  const int ncol = M + nx;
-  for (int col0 = 0; col0 < ncol; col0 += kWave) {
-    const int l = col0 + lane;
-    double acc[MAXM];
+  // QR of the weighted least-squares matrix W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens
+  // rotations, carrying the right-hand block V = [Q^1/2 Phi_dev; 0]  (the
+  // normal equations G'QG + Lambda reach cond 1e12 on the config-2 grid and lose ~1e-5).
+  // Lane l owns column l of [R | T] (l < M: R, else T = Q1'V); rotation k is decided by lane k
+  // and broadcast with a wave shuffle.  The Lambda^1/2 rows are already triangular: R0 = Lambda^1/2.
+  const int ncol = M + nx;  // <= 64 (checked on the host)
+  const int l = lane;
+  double rc[MAXM];
+  {
+    double wl0 = 0.0;
+    if (l < M) {
+      const double ln = fabs(lm[l / Nu]);
+      wl0 = sc.wsq ? ln : sqrt(ln);
+    }
 #pragma unroll
-    for (int a = 0; a < MAXM; ++a) acc[a] = 0.0;
-    if (l < ncol) {
-      for (int i = 0; i < my; ++i) {
-        const double di = fabs(dl[i]);
-        const double wi = sc.wsq ? di * di : di;
-        const int n1 = sc.n1[i];
-        const double* stp = sstep + i * nu * sc.tlen;
-        for (int r = 0; r < N2; ++r) {
-          double cv;
-          if (l < M) {
-            int n = l / Nu, cc = l - n * Nu, tt = n1 + r - cc;
-            cv = tt >= 0 ? stp[n * sc.tlen + tt] : 0.0;
-          } else {
-            cv = sc.phi[(long long)(i * sc.n2max + r) * nx + (l - M)];
-          }
-          cv *= wi;
-          int n = 0, cc = 0;
+    for (int k = 0; k < MAXM; ++k) rc[k] = (k == l) ? wl0 : 0.0;
+  }
+  for (int i = 0; i < my; ++i) {
+    const double di = fabs(dl[i]);
+    const double sqi = sc.wsq ? di : sqrt(di);
+    const int n1 = sc.n1[i];
+    const double* stp = sstep + i * nu * sc.tlen;
+    for (int r = 0; r < N2; ++r) {
+      double w = 0.0;
+      if (l < M) {
+        const int n = l / Nu, cc = l - n * Nu, tt = n1 + r - cc;
+        w = tt >= 0 ? stp[n * sc.tlen + tt] : 0.0;
+      } else if (l < ncol) {
+        w = sc.phi[(long long)(i * sc.n2max + r) * nx + (l - M)];
+      }
+      w *= sqi;
 #pragma unroll
-          for (int a = 0; a < MAXM; ++a) {
-            if (a < M) {
-              int tt = n1 + r - cc;
-              double g = tt >= 0 ? stp[n * sc.tlen + tt] : 0.0;
-              acc[a] += g * cv;
-              if (++cc == Nu) {
-                cc = 0;
-                ++n;
-              }
-            }
+      for (int k = 0; k < MAXM; ++k) {
+        if (k < M) {
+          const double b = __shfl(w, k, 64);
+          if (b != 0.0) {
+            const double a = __shfl(rc[k], k, 64);
+            const double rho = sqrt(a * a + b * b);
+            const double cs = a / rho, sn = b / rho;
+            const double rk = rc[k];
+            rc[k] = cs * rk + sn * w;
+            w = -sn * rk + cs * w;
           }
         }
       }
-      if (l < M) {
-        const int n = l / Nu;
-        const double ln = fabs(lm[n]);
-        const double wl = sc.wsq ? ln * ln : ln;
-#pragma unroll
-        for (int a = 0; a < MAXM; ++a)
-          if (a < M) sH[a * M + l] = acc[a] + (a == l ? wl : 0.0);
-      } else {
-        const int s = l - M;
-#pragma unroll
-        for (int a = 0; a < MAXM; ++a)
-          if (a < M) sA[s * M + a] = acc[a];
-      }
     }
   }
-  __syncthreads();
-  // symmetrise H (S1 = (S1+S1')/2, DTC_GPC_WW.m:99), Cholesky in place (lower), lanes = rows
-  for (int e = lane; e < M * M; e += kWave) {
-    int a = e / M, b = e - a * M;
-    if (a > b) {
-      double h = 0.5 * (sH[a * M + b] + sH[b * M + a]);
-      sH[a * M + b] = h;
-      sH[b * M + a] = h;
-    }
+  // R to LDS (row-major, upper); singular R -> non-finite status
+  if (l < M) {
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+      if (k < M) sH[k * M + l] = rc[k];
   }
   __syncthreads();
   bool spd = true;
-  for (int k = 0; k < M; ++k) {
-    double dkk = sH[k * M + k];
-    if (!(dkk > 0.0)) spd = false;
-    double dsq = sqrt(dkk);
-    __syncthreads();
-    if (lane == 0) sH[k * M + k] = dsq;
-    for (int i = k + 1 + lane; i < M; i += kWave) sH[i * M + k] /= dsq;
-    __syncthreads();
-    for (int i = k + 1 + lane; i < M; i += kWave) {
-      double lik = sH[i * M + k];
-      for (int j = k + 1; j <= i; ++j) sH[i * M + j] -= lik * sH[j * M + k];
-    }
-    __syncthreads();
-  }
+  for (int k = 0; k < M; ++k)
+    if (!(sH[k * M + k] > 0.0)) spd = false;
   if (!spd) {
     write_nan(MPCT_ST_NONFINITE_);
     return;
   }
-  // A = -H^-1 K by two triangular solves per column (lane = column s), column-major [s][m]
-  for (int s = lane; s < nx; s += kWave) {
-    double w[MAXM];
+  // A = -R^-1 T (lanes M..M+nx-1, own column, back substitution), column-major [s][m]
+  if (l >= M && l < ncol) {
 #pragma unroll
-    for (int b = 0; b < MAXM; ++b) w[b] = b < M ? sA[s * M + b] : 0.0;
+    for (int kk = MAXM - 1; kk >= 0; --kk) {
+      if (kk < M) {
+        double a = rc[kk];
 #pragma unroll
-    for (int i = 0; i < MAXM; ++i) {  // L w = k
-      if (i < M) {
-        double a = w[i];
-#pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k < i) a -= sH[i * M + k] * w[k];
-        w[i] = a / sH[i * M + i];
-      }
-    }
-#pragma unroll
-    for (int ii = MAXM - 1; ii >= 0; --ii) {  // L' x = w
-      if (ii < M) {
-        double a = w[ii];
-#pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k > ii && k < M) a -= sH[k * M + ii] * w[k];
-        w[ii] = a / sH[ii * M + ii];
+        for (int j = 0; j < MAXM; ++j)
+          if (j > kk && j < M) a -= sH[kk * M + j] * rc[j];
+        rc[kk] = a / sH[kk * M + kk];
       }
     }
 #pragma unroll
     for (int m = 0; m < MAXM; ++m)
-      if (m < M) sA[s * M + m] = -w[m];
+      if (m < M) sA[(l - M) * M + m] = -rc[m];
   }
-  __syncthreads();
-  // H^-1 = Linv' Linv for the active-set QP (union region is free: step table no longer needed)
-  double* sT = lds + L.Y;
-  for (int j = lane; j < M; j += kWave) {
-    for (int i = 0; i < M; ++i) sT[i * M + j] = 0.0;
-    for (int i = j; i < M; ++i) {
-      double a = (i == j) ? 1.0 : 0.0;
-      for (int k = j; k < i; ++k) a -= sH[i * M + k] * sT[k * M + j];
-      sT[i * M + j] = a / sH[i * M + i];
+  // R^-1 (upper) for the active-set method: lane j solves R x = e_j
+  double* sRinv = lds + L.Y;  // temporary (union region; step table no longer needed)
+  if (l < M) {
+    double x[MAXM];
+#pragma unroll
+    for (int kk = 0; kk < MAXM; ++kk) x[kk] = 0.0;
+#pragma unroll
+    for (int kk = MAXM - 1; kk >= 0; --kk) {
+      if (kk < M) {
+        double a = (kk == l) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < MAXM; ++j)
+          if (j > kk && j < M) a -= sH[kk * M + j] * x[j];
+        x[kk] = (kk <= l) ? a / sH[kk * M + kk] : 0.0;
+      }
     }
+#pragma unroll
+    for (int kk = 0; kk < MAXM; ++kk)
+      if (kk < M) sRinv[kk * M + l] = x[kk];
   }
   __syncthreads();
-  double* sHi = lds + L.sinv;
-  for (int e = lane; e < M * M; e += kWave) {
-    int a = e / M, b = e - a * M;
-    int k0 = a > b ? a : b;
-    double acc = 0.0;
-    for (int k = k0; k < M; ++k) acc += sT[k * M + a] * sT[k * M + b];
-    sHi[e] = acc;
-  }
-  __syncthreads();
-  for (int e = lane; e < M * M; e += kWave) sH[e] = sHi[e];
+  for (int e = lane; e < M * M; e += kWave) sH[e] = sRinv[e];
   __syncthreads();
 
   const double* bnd = sc.bnd;
@@ -507,7 +507,7 @@ __global__ void __launch_bounds__(64)
       sxc[lane] = a0 + a1;
     }
     __syncthreads();
-    iters += gi_qp(lds, L, M, Nu, nu, bnd, tol, maxit, &st);
+    iters += gi_qp<MAXM>(lds, L, M, Nu, nu, bnd, tol, maxit, &st);
   };
 
   // ------------------------------------------------------------------ open-loop prediction

@@ -184,6 +184,10 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     delete s;
     return fail(MPCT_ERANGE, "free-response state too large");
   }
+  if (nu * s->numax + s->nx > kWave) {
+    delete s;
+    return fail(MPCT_ERANGE, "nu*nu_max + free-response state must fit one wavefront (<= 64 columns)");
+  }
   // ---- Diophantine + deltaUFree per output (window rows j = n1_i .. n1_i + N - 1)
   s->phi.assign((size_t)my * N * s->nx, 0.0);
   for (int i = 0; i < my; ++i) {

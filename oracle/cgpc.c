@@ -5,13 +5,14 @@
  *
  * Per candidate (closedloop_toolbox.m:36-100 semantics):
  *   G[(i,r),(n,c)] = s_in(n1_i + r - c)              MatG.m:64-67 (step table from the caller)
- *   H = G'QG + Lambda, Cholesky                       DTC_GPC_WW.m:98-100 (Q, Lambda squared
- *                                                     when the toolbox cost is selected)
+ *   W = [Q^1/2 G; Lambda^1/2] = Q1 R by row-streamed Givens (R'R = H = G'QG + Lambda of
+ *   DTC_GPC_WW.m:98-100, never formed: the normal equations lose ~cond(H)*eps)
+ *   B = -R^-1 Q1'[Q^1/2; 0]                           (unconstrained minimiser dU = B (f - w))
  * per step t:
  *   y(t)        exact difference equations of every plant entry (lsim)
  *   f = Phi x   Phi = [F | Hp] rows, x = [y histories | du histories]   DTC_GPC_WW.m:139-146
- *   g = G'Q(f - r(t))                                   reference held flat (RefLookAhead off)
- *   dU = argmin 1/2 dU'H dU + g'dU s.t. rate/amplitude bounds: unconstrained Cholesky solve, then
+ *   dU = B (f - r(t))                                   reference held flat (RefLookAhead off)
+ *   dU = argmin 1/2 dU'H dU + g'dU s.t. rate/amplitude bounds: unconstrained minimiser, then
  *        a Goldfarb-Idnani dual active-set method (same family as the toolbox's KWIK solver)
  *   u(t) = u(t-1) + dU(first move of every MV)
  * Costs: J1 (GAM_fun.m:219-220), j22 from inK (VNS2.m:173,177); open loop (uopt, ys, j21, Jnu)
@@ -47,44 +48,6 @@ typedef struct {
 
 #define CG_MAXM 64
 
-static void chol(double* A, int n, int* ok) { /* lower, in place */
-  *ok = 1;
-  for (int k = 0; k < n; ++k) {
-    double d = A[k * n + k];
-    for (int j = 0; j < k; ++j) d -= A[k * n + j] * A[k * n + j];
-    if (!(d > 0)) {
-      *ok = 0;
-      return;
-    }
-    d = sqrt(d);
-    A[k * n + k] = d;
-    for (int i = k + 1; i < n; ++i) {
-      double s = A[i * n + k];
-      for (int j = 0; j < k; ++j) s -= A[i * n + j] * A[k * n + j];
-      A[i * n + k] = s / d;
-    }
-  }
-}
-
-/* H^-1 from the Cholesky factor */
-static void chol_inv(const double* Lc, int n, double* Hi) {
-  double* Li = (double*)calloc((size_t)n * n, sizeof(double));
-  for (int j = 0; j < n; ++j)
-    for (int i = j; i < n; ++i) {
-      double s = (i == j) ? 1.0 : 0.0;
-      for (int k = j; k < i; ++k) s -= Lc[i * n + k] * Li[k * n + j];
-      Li[i * n + j] = s / Lc[i * n + i];
-    }
-  for (int a = 0; a < n; ++a)
-    for (int b = 0; b < n; ++b) {
-      int k0 = a > b ? a : b;
-      double s = 0;
-      for (int k = k0; k < n; ++k) s += Li[k * n + a] * Li[k * n + b];
-      Hi[a * n + b] = s;
-    }
-  free(Li);
-}
-
 /* constraint p = 4*m + kind; see gpc_kernel.hip for the same convention */
 static double slack(const double* x, int p, int Nu, const double* bnd, const double* up, int nu) {
   int m = p >> 2, kind = p & 3, n = m / Nu, l = m - n * Nu;
@@ -109,11 +72,18 @@ static void normal_range(int p, int Nu, int* j0, int* j1, double* sg) {
   *j1 = m;
 }
 
-/* Goldfarb-Idnani (Schur form), x holds the unconstrained minimiser on entry */
-static int gi_qp(const double* Hi, int M, int Nu, int nu, const double* bnd, const double* up,
+/* Goldfarb-Idnani dual active-set method in its numerically stable form (the toolbox's KWIK is
+ * of this family).  With H = R'R (R from the QR of W) and B = R^-T N_W for the active normals:
+ *   b_p = R^-T n_p,  [c; tail] = Qb' b_p (Householder QR of B, recomputed every iteration),
+ *   r = Rb^-1 c (dual direction),  e = b_p - B r = Qb [0; tail],  z = R^-1 e (primal direction),
+ *   beta = n_p' z = |tail|^2.
+ * x holds the unconstrained minimiser on entry.  Rinv is upper triangular, row-major. */
+static int gi_qp(const double* Rinv, int M, int Nu, int nu, const double* bnd, const double* up,
                  double* x, double tol, int maxit, int* st) {
-  double Y[CG_MAXM * CG_MAXM], S[CG_MAXM * CG_MAXM], T[CG_MAXM * CG_MAXM];
-  double v[CG_MAXM], z[CG_MAXM], r[CG_MAXM], u[CG_MAXM], sv[CG_MAXM];
+  double Bc[CG_MAXM * CG_MAXM]; /* active b_w columns [w][m] */
+  double Aw[CG_MAXM * (CG_MAXM + 1)]; /* work: column-major [col][m] */
+  double V[CG_MAXM * CG_MAXM], vnv[CG_MAXM];
+  double bp[CG_MAXM], e[CG_MAXM], z[CG_MAXM], r[CG_MAXM], u[CG_MAXM];
   int W[CG_MAXM];
   unsigned char act[4 * CG_MAXM];
   memset(act, 0, sizeof(act));
@@ -130,46 +100,69 @@ static int gi_qp(const double* Hi, int M, int Nu, int nu, const double* bnd, con
       }
     }
     if (!(best < -tol)) break;
-    if (it >= maxit) {
+    if (it >= maxit || q >= M) {
       *st |= 1;
       break;
     }
     int j0, j1;
     double sg;
     normal_range(p, Nu, &j0, &j1, &sg);
+    double bpn = 0.0;
+    for (int m = 0; m < M; ++m) {
+      double a = 0;
+      for (int j = j0; j <= j1; ++j) a += Rinv[j * M + m];
+      bp[m] = sg * a;
+      bpn += bp[m] * bp[m];
+    }
     double sp = best, upm = 0.0;
     for (;;) {
       ++it;
+      /* Householder QR of [B | b_p] */
+      for (int w = 0; w < q; ++w) memcpy(Aw + w * M, Bc + w * M, sizeof(double) * M);
+      memcpy(Aw + q * M, bp, sizeof(double) * M);
+      for (int j = 0; j < q; ++j) {
+        double* cj = Aw + j * M;
+        double nrm = 0;
+        for (int k = j; k < M; ++k) nrm += cj[k] * cj[k];
+        nrm = sqrt(nrm);
+        double alpha = cj[j] > 0 ? -nrm : nrm;
+        double* v = V + j * M;
+        for (int k = 0; k < M; ++k) v[k] = k < j ? 0.0 : cj[k];
+        v[j] -= alpha;
+        double vn = 0;
+        for (int k = j; k < M; ++k) vn += v[k] * v[k];
+        vnv[j] = vn;
+        for (int w = j; w <= q; ++w) {
+          double* cw = Aw + w * M;
+          if (vn == 0.0) continue;
+          double dt = 0;
+          for (int k = j; k < M; ++k) dt += v[k] * cw[k];
+          double f = 2.0 * dt / vn;
+          for (int k = j; k < M; ++k) cw[k] -= f * v[k];
+        }
+      }
+      double* cq = Aw + q * M;
+      double beta = 0;
+      for (int k = q; k < M; ++k) beta += cq[k] * cq[k];
+      for (int k = 0; k < M; ++k) e[k] = k < q ? 0.0 : cq[k];
+      for (int j = q - 1; j >= 0; --j) {
+        const double* v = V + j * M;
+        if (vnv[j] == 0.0) continue;
+        double dt = 0;
+        for (int k = j; k < M; ++k) dt += v[k] * e[k];
+        double f = 2.0 * dt / vnv[j];
+        for (int k = j; k < M; ++k) e[k] -= f * v[k];
+      }
+      for (int w = q - 1; w >= 0; --w) { /* Rb r = c */
+        double a = cq[w];
+        for (int k = w + 1; k < q; ++k) a -= Aw[k * M + w] * r[k];
+        r[w] = a / Aw[w * M + w];
+      }
       for (int m = 0; m < M; ++m) {
         double a = 0;
-        for (int j = j0; j <= j1; ++j) a += Hi[j * M + m];
-        v[m] = sg * a;
-      }
-      for (int w = 0; w < q; ++w) {
-        int a0, a1;
-        double sw;
-        normal_range(W[w], Nu, &a0, &a1, &sw);
-        double a = 0;
-        for (int j = a0; j <= a1; ++j) a += v[j];
-        sv[w] = sw * a;
-      }
-      for (int w = 0; w < q; ++w) {
-        double a = 0;
-        for (int k = 0; k < q; ++k) a += S[w * M + k] * sv[k];
-        r[w] = a;
-      }
-      for (int m = 0; m < M; ++m) {
-        double a = v[m];
-        for (int w = 0; w < q; ++w) a -= Y[w * M + m] * r[w];
+        for (int k = m; k < M; ++k) a += Rinv[m * M + k] * e[k];
         z[m] = a;
       }
-      double beta = 0, cpp = 0;
-      for (int j = j0; j <= j1; ++j) {
-        beta += z[j];
-        cpp += v[j];
-      }
-      beta *= sg;
-      cpp *= sg;
       double t1 = INFINITY;
       int kd = -1;
       for (int w = 0; w < q; ++w)
@@ -177,7 +170,7 @@ static int gi_qp(const double* Hi, int M, int Nu, int nu, const double* bnd, con
           t1 = u[w] / r[w];
           kd = w;
         }
-      double t2 = (beta > 1e-14 * cpp) ? -sp / beta : INFINITY;
+      double t2 = (beta > 1e-14 * bpn) ? -sp / beta : INFINITY;
       if (t1 == INFINITY && t2 == INFINITY) {
         *st |= 2;
         return it;
@@ -190,44 +183,19 @@ static int gi_qp(const double* Hi, int M, int Nu, int nu, const double* bnd, con
       upm += t;
       sp += t * beta;
       if (full) {
-        for (int m = 0; m < M; ++m) Y[q * M + m] = v[m];
-        double ib = 1.0 / beta;
-        for (int a = 0; a <= q; ++a)
-          for (int b = 0; b <= q; ++b) {
-            double val;
-            if (a < q && b < q)
-              val = S[a * M + b] + r[a] * r[b] * ib;
-            else if (a < q)
-              val = -r[a] * ib;
-            else if (b < q)
-              val = -r[b] * ib;
-            else
-              val = ib;
-            T[a * M + b] = val;
-          }
-        for (int a = 0; a <= q; ++a)
-          for (int b = 0; b <= q; ++b) S[a * M + b] = T[a * M + b];
+        memcpy(Bc + q * M, bp, sizeof(double) * M);
         u[q] = upm;
         W[q] = p;
         act[p] = 1;
         ++q;
         break;
       }
-      /* drop kd */
+      /* drop kd (keep order) */
       act[W[kd]] = 0;
-      double ikk = 1.0 / S[kd * M + kd];
-      for (int a = 0; a < q; ++a)
-        for (int b = 0; b < q; ++b) {
-          if (a == kd || b == kd) continue;
-          int na = (a == q - 1) ? kd : a, nb = (b == q - 1) ? kd : b;
-          T[na * M + nb] = S[a * M + b] - S[a * M + kd] * S[kd * M + b] * ikk;
-        }
-      for (int a = 0; a < q - 1; ++a)
-        for (int b = 0; b < q - 1; ++b) S[a * M + b] = T[a * M + b];
-      if (kd != q - 1) {
-        for (int m = 0; m < M; ++m) Y[kd * M + m] = Y[(q - 1) * M + m];
-        u[kd] = u[q - 1];
-        W[kd] = W[q - 1];
+      for (int w = kd; w < q - 1; ++w) {
+        memcpy(Bc + w * M, Bc + (w + 1) * M, sizeof(double) * M);
+        u[w] = u[w + 1];
+        W[w] = W[w + 1];
       }
       --q;
       if (it >= maxit) {
@@ -249,52 +217,72 @@ static int simulate(const cg_scen* sc, int N2, int Nu, const double* delta, cons
   const int M = nu * Nu, P = my * N2;
   if (M > CG_MAXM || N2 > sc->n2max || Nu > N2 || Nu < 1) return 16;
   double* G = (double*)calloc((size_t)P * M, sizeof(double));
-  double* QG = (double*)calloc((size_t)P * M, sizeof(double));
-  double* H = (double*)calloc((size_t)M * M, sizeof(double));
-  double* Hi = (double*)calloc((size_t)M * M, sizeof(double));
+  double* RT = (double*)calloc((size_t)M * (M + P), sizeof(double)); /* [R | T] rows */
+  double* B = (double*)calloc((size_t)M * P, sizeof(double));
+  double* Hi = (double*)calloc((size_t)M * M, sizeof(double)); /* R^-1 */
   double* f = (double*)calloc((size_t)P, sizeof(double));
   double* xs = (double*)calloc((size_t)nx, sizeof(double));
   double* U = (double*)calloc((size_t)2 * nin * nit, sizeof(double)); /* [copy][j][t] */
   double* Ye = (double*)calloc((size_t)2 * sc->ne * nit, sizeof(double));
-  double qw[64], g[CG_MAXM], x[CG_MAXM], ucum[CG_MAXM];
+  double* row = (double*)calloc((size_t)(M + P), sizeof(double));
+  double sqw[64], x[CG_MAXM], ucum[CG_MAXM];
   int st = 0;
   int64_t iters = 0;
+  const int ncol = M + P;
   for (int i = 0; i < my; ++i) {
     double d = fabs(delta[i]);
-    qw[i] = sc->wsq ? d * d : d;
+    sqw[i] = sc->wsq ? d : sqrt(d); /* Q^1/2 */
   }
   for (int i = 0; i < my; ++i)
     for (int rr = 0; rr < N2; ++rr)
       for (int n = 0; n < nu; ++n)
         for (int c = 0; c < Nu; ++c) {
           int t = sc->n1[i] + rr - c;
-          double gv = t >= 0 ? sc->step[((size_t)i * nu + n) * sc->tlen + t] : 0.0;
-          G[(size_t)(i * N2 + rr) * M + n * Nu + c] = gv;
-          QG[(size_t)(i * N2 + rr) * M + n * Nu + c] = qw[i] * gv;
+          G[(size_t)(i * N2 + rr) * M + n * Nu + c] = t >= 0 ? sc->step[((size_t)i * nu + n) * sc->tlen + t] : 0.0;
         }
-  for (int a = 0; a < M; ++a)
-    for (int b = 0; b < M; ++b) {
-      double s = 0;
-      for (int k = 0; k < P; ++k) s += G[(size_t)k * M + a] * QG[(size_t)k * M + b];
-      H[a * M + b] = s;
-    }
-  for (int a = 0; a < M; ++a)
-    for (int b = 0; b < a; ++b) {
-      double h = 0.5 * (H[a * M + b] + H[b * M + a]);
-      H[a * M + b] = H[b * M + a] = h;
-    }
+  /* QR of W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens rotations, carrying the right-hand
+   * block V = [diag(Q^1/2); 0]:  R starts as Lambda^1/2 (already triangular), T = Q1'V. */
   for (int n = 0; n < nu; ++n) {
     double l = fabs(lam[n]);
-    double w = sc->wsq ? l * l : l;
-    for (int c = 0; c < Nu; ++c) H[(n * Nu + c) * M + n * Nu + c] += w;
+    double w = sc->wsq ? l : sqrt(l);
+    for (int c = 0; c < Nu; ++c) RT[(size_t)(n * Nu + c) * ncol + n * Nu + c] = w;
   }
-  int ok;
-  chol(H, M, &ok);
-  if (!ok) {
-    st |= 4;
-    goto done;
+  for (int k = 0; k < P; ++k) {
+    const double q = sqw[k / N2];
+    memset(row, 0, sizeof(double) * ncol);
+    for (int a = 0; a < M; ++a) row[a] = q * G[(size_t)k * M + a];
+    row[M + k] = q;
+    for (int a = 0; a < M; ++a) {
+      double bb = row[a];
+      if (bb == 0.0) continue;
+      double aa = RT[(size_t)a * ncol + a];
+      double rho = hypot(aa, bb), cs = aa / rho, sn = bb / rho;
+      for (int j = a; j < ncol; ++j) {
+        double rj = RT[(size_t)a * ncol + j], wj = row[j];
+        RT[(size_t)a * ncol + j] = cs * rj + sn * wj;
+        row[j] = -sn * rj + cs * wj;
+      }
+    }
   }
-  chol_inv(H, M, Hi);
+  for (int a = 0; a < M; ++a)
+    if (!(RT[(size_t)a * ncol + a] > 0.0)) {
+      st |= 4;
+      goto done;
+    }
+  /* B = -R^-1 T  (M x P) */
+  for (int k = 0; k < P; ++k)
+    for (int a = M - 1; a >= 0; --a) {
+      double acc = RT[(size_t)a * ncol + M + k];
+      for (int j = a + 1; j < M; ++j) acc -= RT[(size_t)a * ncol + j] * (-B[(size_t)j * P + k]);
+      B[(size_t)a * P + k] = -acc / RT[(size_t)a * ncol + a];
+    }
+  /* R^-1 (upper) for the active-set method */
+  for (int j = 0; j < M; ++j)
+    for (int a = j; a >= 0; --a) {
+      double acc = (a == j) ? 1.0 : 0.0;
+      for (int k = a + 1; k <= j; ++k) acc -= RT[(size_t)a * ncol + k] * Hi[(size_t)k * M + j];
+      Hi[(size_t)a * M + j] = acc / RT[(size_t)a * ncol + a];
+    }
   {
     const double tol = 1e-10;
     const int maxit = 8 * M + 16;
@@ -313,12 +301,7 @@ static int simulate(const cg_scen* sc, int N2, int Nu, const double* delta, cons
       }                                                                        \
     for (int a = 0; a < M; ++a) {                                              \
       double s = 0;                                                            \
-      for (int k = 0; k < P; ++k) s += QG[(size_t)k * M + a] * f[k];           \
-      g[a] = s;                                                                \
-    }                                                                          \
-    for (int a = 0; a < M; ++a) {                                              \
-      double s = 0;                                                            \
-      for (int b = 0; b < M; ++b) s -= Hi[a * M + b] * g[b];                   \
+      for (int k = 0; k < P; ++k) s += B[(size_t)a * P + k] * f[k];            \
       x[a] = s;                                                                \
     }                                                                          \
     iters += gi_qp(Hi, M, Nu, nu, bnd, uprev, x, tol, maxit, &st);             \
@@ -410,8 +393,9 @@ static int simulate(const cg_scen* sc, int N2, int Nu, const double* delta, cons
 done:
   if (iters_out) *iters_out = iters;
   free(G);
-  free(QG);
-  free(H);
+  free(RT);
+  free(B);
+  free(row);
   free(Hi);
   free(f);
   free(xs);

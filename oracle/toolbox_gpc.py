@@ -17,9 +17,10 @@ primitives A3-A8 (arithmetic):
   window='toolbox' predicts t+1..t+N2 (toolbox), window='gpc' predicts t+dmin+1..t+dmin+N2
   (MatG/diophantine N1 = d+1), weights_squared=False gives the DTC_GPC_WW.m:67-76 weighting.
 * The per-step QP  min 1/2 dU'(G'QG + Lambda) dU + dU'G'Q(f - w)  is solved to optimality by a
-  textbook primal active-set method (Nocedal & Wright Alg. 16.3) — deliberately a different
-  algorithm from the device's dual (Goldfarb-Idnani) method; the strictly convex QP has a
-  unique minimiser, so both must agree to rounding.
+  textbook primal active-set method (Nocedal & Wright Alg. 16.3) on its least-squares form
+  ||[Q^1/2 G; Lambda^1/2] dU + [Q^1/2 (f-w); 0]||^2 (never forming the ill-conditioned normal
+  equations) — deliberately a different algorithm from the device's dual (Goldfarb-Idnani)
+  method; the strictly convex QP has a unique minimiser, so both must agree to rounding.
 * Open-loop first-move prediction (closedloop_toolbox.m:85-100): the QP at the initial state
   with reference r(:,end) gives Info.Uopt (p+1 rows, held after the control horizon), padded
   with its last row to nit (:94-98); ys = lsim(Pz, [uopt v]) (:100).
@@ -125,51 +126,67 @@ def constraint_rows(nu: int, Nu: int, du_min, du_max, u_min, u_max, u_prev):
     return np.array(rows), np.array(rhs)
 
 
-def qp_primal_active_set(H, g, Ain, bin_, tol=1e-12, maxit=1000):
-    """min 1/2 x'Hx + g'x  s.t. Ain x >= bin, from the feasible start x = 0 (Nocedal & Wright
-    Alg. 16.3).  Returns (x, iterations, working_set, multipliers)."""
-    M = H.shape[0]
+def qp_primal_active_set(W, c, Ain, bin_, tol=1e-12, maxit=1000):
+    """min 1/2 ||W x + c||^2  s.t. Ain x >= bin, from the feasible start x = 0 — a textbook
+    primal active-set method (Nocedal & Wright Alg. 16.3) that never forms the normal equations:
+    the equality-constrained subproblem on the working set is solved by the null-space method,
+    p = Z y, y = lstsq(W Z, -(W x + c)) (SVD), Z an orthonormal basis of null(Ain[W]).
+    H = W'W, g = W'c is the toolbox QP min 1/2 dU'H dU + g'dU.  Normal equations would lose
+    ~cond(H)*eps (~1e-5 at cond 1e11, reached on the config-2 grid); see DESIGN.md §Numerics.
+    Returns (x, iterations, working_set, multipliers)."""
+    M = W.shape[1]
     x = np.zeros(M)
     s = Ain @ x - bin_ if Ain.size else np.zeros(0)
     if Ain.size and np.any(s < -1e-9):
         raise ValueError("QP start point infeasible (%g)" % s.min())
-    W = []
+    W_ = []
     for i in np.nonzero(s <= tol)[0]:  # independent initial working set
-        cand = W + [int(i)]
+        cand = W_ + [int(i)]
         if np.linalg.matrix_rank(Ain[cand]) == len(cand):
-            W = cand
+            W_ = cand
     it = 0
     while it < maxit:
         it += 1
-        q = len(W)
-        K = np.zeros((M + q, M + q))
-        K[:M, :M] = H
+        q = len(W_)
+        res = W @ x + c
         if q:
-            AW = Ain[W]
-            K[:M, M:] = -AW.T
-            K[M:, :M] = AW
-        rhs = np.concatenate([-(H @ x + g), np.zeros(q)])
-        sol = np.linalg.solve(K, rhs)
-        p = sol[:M]
-        mu = sol[M:]  # multipliers at x + p: H(x+p) + g = A_W' mu
+            AW = Ain[W_]
+            _, sv, Vt = np.linalg.svd(AW)
+            Z = Vt[q:].T
+        else:
+            Z = np.eye(M)
+        if Z.shape[1]:
+            y = np.linalg.lstsq(W @ Z, -res, rcond=None)[0]
+            p = Z @ y
+        else:
+            p = np.zeros(M)
         alpha, block = 1.0, None
         if Ain.size:
             Ap = Ain @ p
             s = Ain @ x - bin_
+            # only a constraint the step really moves toward can block it; a rounding-level
+            # A_i p < 0 would admit a constraint dependent on the working set (degenerate cycling)
+            thr = 1e-12 * np.max(np.abs(p)) * np.max(np.abs(Ain), axis=1)
             for i in range(Ain.shape[0]):
-                if i in W or Ap[i] >= -1e-300:
+                if i in W_ or Ap[i] >= -thr[i]:
                     continue
                 a = max(s[i], 0.0) / (-Ap[i])
                 if a < alpha:
                     alpha, block = a, i
         x = x + alpha * p
         if block is not None:
-            W.append(block)
+            W_.append(block)
             continue
-        # full step: x is the minimiser on the working set; check the multipliers
-        if q == 0 or np.all(mu >= -1e-12 * (1.0 + np.max(np.abs(mu)))):
-            return x, it, W, mu
-        W.pop(int(np.argmin(mu)))
+        # full step: x minimises on the working set; multipliers from W'(Wx + c) = AW' mu
+        if q == 0:
+            return x, it, W_, np.zeros(0)
+        grad = W.T @ (W @ x + c)
+        mu = np.linalg.lstsq(Ain[W_].T, grad, rcond=None)[0]
+        # scale-relative optimality test: the multipliers scale with the objective, which can be
+        # ~1e-9 on the config-2 grid (an absolute tolerance accepts wrong working sets there)
+        if np.all(mu >= -1e-9 * np.max(np.abs(mu))):
+            return x, it, W_, mu
+        W_.pop(int(np.argmin(mu)))
     raise RuntimeError("primal active set did not converge")
 
 
@@ -249,9 +266,9 @@ def closedloop_toolbox(sc: Scenario, r, v, N2: int, Nu: int, delta, lam, nit: in
     wq = delta ** 2 if sc.weights_squared else delta
     wl = lam ** 2 if sc.weights_squared else lam
     qdiag = np.repeat(wq, N2)
-    H = G.T @ (qdiag[:, None] * G) + np.diag(np.repeat(wl, Nu))
-    H = 0.5 * (H + H.T)
-    GtQ = G.T * qdiag[None, :]
+    # weighted least-squares form of the toolbox cost: ||Q^1/2 (G dU + f - w)||^2 + ||Lambda^1/2 dU||^2
+    sq = np.sqrt(qdiag)
+    Wls = np.vstack([sq[:, None] * G, np.diag(np.sqrt(np.repeat(wl, Nu)))])
     na = sc.na
     M = nu * Nu
     plant = _Plant(sc.plant)
@@ -260,9 +277,9 @@ def closedloop_toolbox(sc: Scenario, r, v, N2: int, Nu: int, delta, lam, nit: in
         Yd = np.concatenate([yhist[i] for i in range(my)])
         f = Hp @ up + S @ Yd
         w = np.repeat(rvec, N2)
-        g = GtQ @ (f - w)
+        cvec = np.concatenate([sq * (f - w), np.zeros(M)])
         Ain, bin_ = constraint_rows(nu, Nu, sc.du_min, sc.du_max, sc.u_min, sc.u_max, u_prev)
-        x, it, _, _ = qp_primal_active_set(H, g, Ain, bin_)
+        x, it, _, _ = qp_primal_active_set(Wls, cvec, Ain, bin_)
         return x, it
 
     ys = uopt = None

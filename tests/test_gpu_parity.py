@@ -143,10 +143,14 @@ def test_full_grid_properties(env):
     perm = np.random.default_rng(1).permutation(4096)
     c = eval_batch(env["sc"], N2[perm], Nu[perm], d[perm], l[perm], env["r"][None])
     assert np.array_equal(c.J1, a.J1[perm])
-    # a sample of the batch against the C port
-    idx = np.arange(0, 4096, 97)
-    ref = env["cp"].eval(N2[idx], Nu[idx], d[idx], l[idx], env["r"][None])
-    assert _rel(a.J1[idx], ref["J1"]) < COST_RTOL
+    # the whole batch against the C port (same stable QR / dual active-set arithmetic on the CPU)
+    ref = env["cp"].eval(N2, Nu, d, l, env["r"][None], threads=16)
+    rel = np.max(np.abs(a.J1 - ref["J1"]) / np.maximum(np.abs(ref["J1"]), 1e-12), axis=1)
+    print("full grid J1: max rel %.2e, 99.9%% %.2e" % (rel.max(), np.quantile(rel, 0.999)))
+    assert rel.max() < COST_RTOL, (int(np.argmax(rel)), rel.max())
+    w = np.array([0.05, 0.40, 0.55])
+    from mpct.objectives import rank
+    assert np.array_equal(rank(a.J1 @ w), rank(ref["J1"] @ w))
 
 
 def test_status_edges(env):
