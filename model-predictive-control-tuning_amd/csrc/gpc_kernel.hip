@@ -2,63 +2,119 @@
 //
 // Replaces, per simulation, the body of closedloop_toolbox.m:36-100 (sim + mpcstate/mpcmove +
 // lsim) with the toolbox-equivalent GPC of DESIGN.md:
-//   prologue (once per candidate):  G from the step table (MatG.m:64-67), H = G'QG + Lambda,
-//       K = G'Q*Phi with Phi = [F | Hp] (diophantine.m / deltaUFree.m / cell2mat2.m tables built
-//       on the host), Kw = G'Q*E;  Cholesky -> H^-1;  A = [-H^-1 K | H^-1 Kw]
-//   per step t:  plant output (exact difference equations of every (i,j) entry — lsim),
-//       unconstrained minimiser dU = A [x; r(t)] (x = y histories | du histories, i.e. the
-//       state S*Yd + Hp*up of DTC_GPC_WW.m:139-146 folded into A), then a Goldfarb-Idnani dual
-//       active-set QP (the toolbox's KWIK is of this family) when a rate / amplitude bound is
-//       violated, apply the first move of every MV, shift the histories.
-// Lanes: rows of the QP (move index m = n*Nu + l) for the solver; plant entries for the plant;
-// columns of [G | Phi | E] in the prologue.  All state lives in LDS (one wave per workgroup, so
-// __syncthreads() is a single-wave barrier).  Arithmetic is IEEE f64 throughout.
+//   prologue (once per candidate): G from the step table (MatG.m:64-67); QR of the weighted
+//       least-squares matrix W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens rotations carrying
+//       V = [Q^1/2 Phi; 0] (Phi: Diophantine F | deltaUFree/cell2mat2 rows built on the host, on
+//       a backward-difference basis); A = -R^-1 Q1'V (unconstrained gain), R^-1 for the QP.
+//   per step t: plant output (exact difference equations of every (i,j) entry — lsim),
+//       unconstrained minimiser dU = A x (x = [y-r, nabla y .. | du history]: the state of
+//       DTC_GPC_WW.m:139-146 S*Yd + Hp*up), then the Goldfarb-Idnani dual active-set QP (the
+//       toolbox's KWIK is of this family) when a rate / amplitude bound is violated; first move of
+//       every MV applied; histories shifted.
+// Latency design (one wave per simulation, the step loop is a serial recurrence):
+//   * everything a step reads lives in LDS or registers (no global loads in the loop except the
+//     prefetched r(t+1), Yref(t+1));
+//   * scalars are broadcast with v_readlane (SGPR), QP-row reductions use DPP row operations when
+//     M <= 16, the active-set QR runs lanes-as-rows entirely in registers;
+//   * a workgroup is exactly one wave: LDS hand-offs between lanes need only lgkmcnt(0) and a
+//     compiler fence (no s_barrier, no vmcnt drain of the prefetches).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include "mpct_dev.h"
 
+#ifndef MPCT_WAVES_PER_EU
+#define MPCT_WAVES_PER_EU 1
+#endif
 namespace mpct {
 
 struct LdsLayout {
-  int hinv, A, x, xc, v, z, r, u, sv, uprev, yprev, ucum, ye, yeh, uring, Y, sinv, tmp, step, wid, total;
+  int rinv, jd, dv, ra, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, wid, mu, step, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int M, int nxa, int nu, int nin, int ne, int my,
-                                                int tlen) {
+__host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, int ne, int my,
+                                                int tlen, int plb, int pla) {
   LdsLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
-  L.hinv = take(M * M);
-  L.A = take(nxa * M);
-  L.x = take(nxa);
+  L.rinv = take(M * M);
+  L.jd = take(M * M);        // row dumps of J (active-set method)
+  L.dv = take(M);            // d = J'n_p
+  L.ra = take(M * M);        // R_A of the active-set method
+  L.A = take(nx * M);
+  L.x = take(nx);
   L.xc = take(M);
-  L.v = take(M);
-  L.z = take(M);
-  L.r = take(M);
-  L.u = take(M);
-  L.sv = take(M);
   L.uprev = take(nu);
   L.yprev = take(my);
   L.ucum = take(M);
   L.ye = take(2 * ne);
   L.yeh = take(2 * ne * kYeHist);
   L.uring = take(2 * nin * kURing);
+  L.plb = take(ne * plb);
+  L.pla = take(ne * pla);
   L.wid = take(M);
-  // union: loop-only QP workspace | prologue step table
-  int u0 = o;
-  L.Y = u0;
-  L.sinv = u0 + M * M;
-  L.tmp = u0 + 2 * M * M;
-  int loopsz = 3 * M * M;
-  L.step = u0;
-  int stepsz = my * nu * tlen;
-  o = u0 + (loopsz > stepsz ? loopsz : stepsz);
+  L.mu = take(M);
+  L.step = take(my * nu * tlen > M * M ? my * nu * tlen : M * M);  // prologue only
   L.total = (o + 1) & ~1;
   return L;
 }
 
-__device__ __forceinline__ void wave_argmin(double& v, int& id) {
+// ------------------------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ void lds_sync() {
+  // one-wave workgroup: LDS requests of a wave complete in order; wait for this lane's and order
+  // the compiler's memory operations around the hand-off
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double bcast(double v, int src) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// DPP controls: quad_perm(1,0,3,2), quad_perm(2,3,0,1), row_half_mirror, row_mirror
+constexpr int kQx1 = 0xB1, kQx2 = 0x4E, kHalfMirror = 0x141, kMirror = 0x140;
+
+// sum over lanes 0..15 (every lane of row 0 gets it; callers zero inactive lanes)
+__device__ __forceinline__ double row_sum(double v) {
+  v += dppd<kQx1>(v);
+  v += dppd<kQx2>(v);
+  v += dppd<kHalfMirror>(v);
+  v += dppd<kMirror>(v);
+  return v;
+}
+__device__ __forceinline__ void row_argmin_step(double& v, int& id, double pv, int pi) {
+  if (pv < v || (pv == v && pi < id)) {
+    v = pv;
+    id = pi;
+  }
+}
+__device__ __forceinline__ void row_argmin(double& v, int& id) {
+  row_argmin_step(v, id, dppd<kQx1>(v), dppi<kQx1>(id));
+  row_argmin_step(v, id, dppd<kQx2>(v), dppi<kQx2>(id));
+  row_argmin_step(v, id, dppd<kHalfMirror>(v), dppi<kHalfMirror>(id));
+  row_argmin_step(v, id, dppd<kMirror>(v), dppi<kMirror>(id));
+}
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ void wave_argmin64(double& v, int& id) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     double ov = __shfl_xor(v, off, 64);
@@ -70,89 +126,122 @@ __device__ __forceinline__ void wave_argmin(double& v, int& id) {
   }
 }
 
+// reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
+template <int MAXM>
+__device__ __forceinline__ double qsum(double v) {
+  if constexpr (MAXM <= 16) {
+    return bcast(row_sum(v), 0);
+  } else {
+    return wave_sum64(v);
+  }
+}
+template <int MAXM>
+__device__ __forceinline__ void qargmin(double& v, int& id) {
+  if constexpr (MAXM <= 16) {
+    row_argmin(v, id);
+    v = bcast(v, 0);
+    id = __builtin_amdgcn_readlane(id, 0);
+  } else {
+    wave_argmin64(v, id);
+  }
+}
+
 // constraint p = 4*m + kind on move m = n*Nu + l:
 //   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
 //   kind 2:  sum_{l'<=l} du_(n,l') >= u_min - u_prev    kind 3: -sum >= -(u_max - u_prev)
 struct CInfo {
-  int j0, j1;   // index range [j0, j1] of the normal's support
-  double sg;    // sign of the normal
+  int j0, j1;
+  double sg;
 };
 __device__ __forceinline__ CInfo cinfo(int p, int Nu) {
-  int m = p >> 2, kind = p & 3;
+  const int m = p >> 2, kind = p & 3;
   CInfo c;
   c.sg = (kind & 1) ? -1.0 : 1.0;
-  if (kind < 2) {
-    c.j0 = m;
-    c.j1 = m;
-  } else {
-    c.j0 = (m / Nu) * Nu;
-    c.j1 = m;
-  }
+  c.j0 = kind < 2 ? m : (m / Nu) * Nu;
+  c.j1 = m;
   return c;
 }
 
-// Slacks of the 4 constraints owned by lane m (< M); +inf for disabled ones.
-__device__ __forceinline__ void lane_slacks(const double* __restrict__ sxc, int m, int Nu,
-                                            const double* bnd, const double* uprev, int nu,
-                                            double s[4]) {
-  int n = m / Nu, l = m - n * Nu;
-  double dmin = bnd[n], dmax = bnd[nu + n], umin = bnd[2 * nu + n], umax = bnd[3 * nu + n];
-  double up = uprev[n];
-  double xm = sxc[m];
-  if (l == 0) {
-    double lo = fmax(dmin, umin - up), hi = fmin(dmax, umax - up);
-    s[0] = xm - lo;
-    s[1] = hi - xm;
+// per-lane constraint data for QP row m (registers)
+struct RowCons {
+  double dmin, dmax, umin, umax;
+  int n, l;
+};
+
+// slacks of the 4 constraints of row m at x (x in LDS), up = u_prev of the row's MV
+__device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m, const RowCons& rc,
+                                           double up, double s[4]) {
+  const double xm = sxc[m];
+  if (rc.l == 0) {
+    s[0] = xm - fmax(rc.dmin, rc.umin - up);
+    s[1] = fmin(rc.dmax, rc.umax - up) - xm;
     s[2] = INFINITY;
     s[3] = INFINITY;
   } else {
     double pre = 0.0;
-    for (int j = n * Nu; j <= m; ++j) pre += sxc[j];
-    s[0] = xm - dmin;
-    s[1] = dmax - xm;
-    s[2] = pre - (umin - up);
-    s[3] = (umax - up) - pre;
+    for (int j = m - rc.l; j <= m; ++j) pre += sxc[j];
+    s[0] = xm - rc.dmin;
+    s[1] = rc.dmax - xm;
+    s[2] = pre - (rc.umin - up);
+    s[3] = (rc.umax - up) - pre;
   }
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+#ifdef MPCT_PROFILE
+#define PSTAMP(k)                                              \
+  do {                                                         \
+    __builtin_amdgcn_sched_barrier(0);                         \
+    unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
+    pacc[k] += now_ - pprev;                                   \
+    pprev = now_;                                              \
+    __builtin_amdgcn_sched_barrier(0);                         \
+  } while (0)
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
 
-// Goldfarb-Idnani dual active-set QP, numerically stable form:
-// with H = R'R (R from the QR of W = [Q^1/2 G; Lambda^1/2]) and B = R^-T N_W for the active
-// normals, each iteration recomputes the Householder QR of [B | b_p] (lanes = columns):
-//   [c; tail] = Qb' b_p,  r = Rb^-1 c,  e = Qb [0; tail],  z = R^-1 e,  beta = n_p'z = |tail|^2.
-// Starts from the unconstrained minimiser in sxc[0..M).  R^-1 (upper, row-major) is in
-// lds[L.hinv].  Returns inner iterations; sets *st bits.  Wave-uniform control flow.
+// ------------------------------------------------------------------------------------------
+// Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
+// family) in its factored, numerically stable form.  H = R'R;
+// J (M x M) with H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].
+// For the most violated constraint p:  d = J'n_p,  z = J(:,q:) d(q:) (primal direction),
+// r = R_A^-1 d(0:q) (dual direction), beta = n_p'z = |d(q:)|^2.  Adding p rotates d(q:) onto
+// d(q) (Givens, applied to J's columns) and appends d(0:q) to R_A; dropping constraint k
+// re-triangularises R_A with Givens rotations applied to J's columns.
+// Lanes = rows of J (registers); d is distributed (lane k holds d_k) through one LDS dump of
+// the rows in the normal's support; R_A lives in LDS.  Starts from the unconstrained minimiser
+// in sxc.  Wave-uniform control flow.
 template <int MAXM>
-__device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, int nu,
-                     const double* bnd, double tol, int maxit, int* st) {
+__device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const RowCons& rc,
+                     double tol, int maxit, int* st
+#ifdef MPCT_PROFILE
+                     , unsigned long long* pacc, unsigned long long& pprev
+#endif
+                     ) {
   const int lane = threadIdx.x;
-  const double* sRi = lds + L.hinv;
+  const bool row = lane < M;
+  const double* sRi = lds + L.rinv;
   double* sxc = lds + L.xc;
-  double* sbp = lds + L.v;
-  double* se = lds + L.z;
-  double* sr = lds + L.r;
-  double* su = lds + L.u;
-  double* sc_ = lds + L.sv;
-  double* sB = lds + L.Y;     // active b_w columns [w][m]
-  double* sRb = lds + L.sinv; // Rb columns [w][k]
-  double* sV = lds + L.tmp;   // reflectors [j][k]
-  double* suprev = lds + L.uprev;
+  double* sRA = lds + L.ra;  // R_A, row-major with stride M
+  double* sJ = lds + L.jd;   // row dumps of J
+  double* sd = lds + L.dv;   // d
+  double* su = lds + L.mu;
+  const double* suprev = lds + L.uprev;
   int* sW = reinterpret_cast<int*>(lds + L.wid);
-  unsigned act = 0;  // active bits of this lane's 4 constraints
+  unsigned act = 0;  // active bits of this row's 4 constraints
   int q = 0, it = 0;
-  double xm = lane < M ? sxc[lane] : 0.0;
+  bool jinit = false;
+  double Jr[MAXM];
+  double xm = row ? sxc[lane] : 0.0;
+  const double up_row = row ? suprev[rc.n] : 0.0;
   for (;;) {
-    // ---- most violated inactive constraint
     double best = INFINITY;
     int bid = 0x7fffffff;
-    if (lane < M) {
+    if (row) {
       double s[4];
-      lane_slacks(sxc, lane, Nu, bnd, suprev, nu, s);
+      row_slacks(sxc, lane, rc, up_row, s);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (!((act >> k) & 1u) && s[k] < best) {
@@ -160,176 +249,165 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
           bid = 4 * lane + k;
         }
     }
-    wave_argmin(best, bid);
+    qargmin<MAXM>(best, bid);
+    PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
     if (it >= maxit || q >= M) {
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
-    const int p = bid;
-    const CInfo cp = cinfo(p, Nu);
-    // b_p = R^-T n_p:  b_p[m] = sg * sum_{j in S_p} Rinv[j][m]
-    double bpm = 0.0;
-    if (lane < M) {
-      for (int j = cp.j0; j <= cp.j1; ++j) bpm += sRi[j * M + lane];
-      bpm *= cp.sg;
-      sbp[lane] = bpm;
+    if (!jinit) {  // J = R^-1
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k) Jr[k] = (row && k < M) ? sRi[lane * M + k] : 0.0;
+      jinit = true;
     }
-    const double bpn = wave_sum(bpm * bpm);
-    double sp = best;  // current slack of p
-    double up = 0.0;   // its multiplier
-    __syncthreads();
+    const int p = bid;
+    const int mp = p >> 2, kindp = p & 3;
+    const int j0 = kindp < 2 ? mp : mp - __builtin_amdgcn_readlane(rc.l, mp);
+    const double sgp = (kindp & 1) ? -1.0 : 1.0;
+    double sp = best;  // slack of p along the path
+    double upm = 0.0;  // its multiplier
+    bool infeas = false;
     for (;;) {
       ++it;
-      // ---- Householder QR of [B | b_p], lane w holds column w (w < q: b_w, w == q: b_p)
-      double col[MAXM];
-      const double* src = lane < q ? sB + lane * M : sbp;
-#pragma unroll
-      for (int k = 0; k < MAXM; ++k) col[k] = (lane <= q && k < M) ? src[k] : 0.0;
-      for (int j = 0; j < q; ++j) {
-        if (lane == j) {
-          double nrm = 0.0, cj = 0.0;
-#pragma unroll
-          for (int k = 0; k < MAXM; ++k)
-            if (k >= j && k < M) nrm += col[k] * col[k];
-#pragma unroll
-          for (int k = 0; k < MAXM; ++k)
-            if (k == j) cj = col[k];
-          nrm = sqrt(nrm);
-          const double alpha = cj > 0.0 ? -nrm : nrm;
-          double vn = 0.0;
-#pragma unroll
-          for (int k = 0; k < MAXM; ++k) {
-            if (k < M) {
-              double v = k < j ? 0.0 : (k == j ? col[k] - alpha : col[k]);
-              sV[j * M + k] = v;
-              vn += v * v;
-              col[k] = k < j ? col[k] : (k == j ? alpha : 0.0);
-            }
-          }
-          sc_[j] = vn;  // |v_j|^2 (sc_ reused: c is read from the b_p lane later)
-        }
-        __syncthreads();
-        if (lane > j && lane <= q) {
-          const double vn = sc_[j];
-          if (vn != 0.0) {
-            double dt = 0.0;
-#pragma unroll
-            for (int k = 0; k < MAXM; ++k)
-              if (k >= j && k < M) dt += sV[j * M + k] * col[k];
-            const double f = 2.0 * dt / vn;
-#pragma unroll
-            for (int k = 0; k < MAXM; ++k)
-              if (k >= j && k < M) col[k] -= f * sV[j * M + k];
-          }
-        }
-      }
-      // Rb columns to LDS; lane q: c (k < q) and tail (k >= q)
-      if (lane < q) {
+      // d = J'n_p = sg * (sum of J's rows j0..mp)
+      if (lane >= j0 && lane <= mp) {
 #pragma unroll
         for (int k = 0; k < MAXM; ++k)
-          if (k < M) sRb[lane * M + k] = col[k];
+          if (k < M) sJ[lane * M + k] = Jr[k];
       }
-      double beta_part = 0.0;
-      if (lane == q) {
-#pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k < M) {
-            se[k] = k < q ? 0.0 : col[k];
-            if (k >= q) beta_part += col[k] * col[k];
-            if (k < q) sr[k] = col[k];  // c, solved in place below
-          }
+      lds_sync();
+      double dk = 0.0;
+      if (row) {
+        for (int j = j0; j <= mp; ++j) dk += sJ[j * M + lane];
+        dk *= sgp;
+        sd[lane] = dk;
       }
-      const double beta = wave_sum(beta_part);
-      __syncthreads();
-      // e = H_0 ... H_{q-1} [0; tail]   (lanes = components)
-      double ek = lane < M ? se[lane] : 0.0;
-      for (int j = q - 1; j >= 0; --j) {
-        const double vn = sc_[j];
-        const double vk = (lane >= j && lane < M) ? sV[j * M + lane] : 0.0;
-        const double dt = wave_sum(vk * ek);
-        if (vn != 0.0) ek -= (2.0 * dt / vn) * vk;
-      }
-      // r = Rb^-1 c  (column-oriented back substitution, lane k holds c_k)
-      double ck = lane < q ? sr[lane] : 0.0;
-      double rk = 0.0;
-      for (int w = q - 1; w >= 0; --w) {
-        const double rw = __shfl(ck, w, 64) / sRb[w * M + w];
-        if (lane == w) rk = rw;
-        if (lane < w) ck -= sRb[w * M + lane] * rw;
-      }
-      if (lane < M) se[lane] = ek;
-      __syncthreads();
-      // z = R^-1 e
+      const double dn2 = qsum<MAXM>(dk * dk);
+      const double beta = qsum<MAXM>(lane >= q ? dk * dk : 0.0);
+      lds_sync();
+      PSTAMP(PROF_QD);
       double zm = 0.0;
-      if (lane < M) {
-        for (int k = lane; k < M; ++k) zm += sRi[lane * M + k] * se[k];
+      if (row) {
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+          if (k >= q && k < M) zm += Jr[k] * sd[k];
       }
-      // dual step length t1 over active constraints with r_w > 0
+      // r = R_A^-1 d(0:q): column-oriented back substitution, lane w holds r_w
+      double ck = lane < q ? dk : 0.0, rk = 0.0;
+      for (int w = q - 1; w >= 0; --w) {
+        const double rw = bcast(ck, w) / sRA[w * M + w];
+        if (lane == w) rk = rw;
+        if (lane < w) ck -= sRA[lane * M + w] * rw;
+      }
+      // dual step over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
       if (lane < q && rk > 0.0) {
         t1 = su[lane] / rk;
         kdrop = lane;
       }
-      wave_argmin(t1, kdrop);
-      const double t2 = (beta > 1e-14 * bpn) ? -sp / beta : INFINITY;
+      qargmin<MAXM>(t1, kdrop);
+      PSTAMP(PROF_QR);
+      const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
       if (t1 == INFINITY && t2 == INFINITY) {
         *st |= MPCT_ST_QP_INFEAS_;
-        if (lane < M) sxc[lane] = xm;
-        __syncthreads();
-        return it;
+        infeas = true;
+        break;
       }
       const bool full = t2 <= t1;
       const double t = full ? t2 : t1;
-      if (lane < M && t2 != INFINITY) {
+      if (row && t2 != INFINITY) {
         xm += t * zm;
         sxc[lane] = xm;
       }
       if (lane < q) su[lane] -= t * rk;
-      up += t;
+      upm += t;
       sp += t * beta;
-      __syncthreads();
       if (full) {
-        if (lane < M) sB[q * M + lane] = sbp[lane];
-        if (lane == 0) {
-          su[q] = up;
-          sW[q] = p;
-        }
-        if (lane == (p >> 2)) act |= 1u << (p & 3);
-        ++q;
-        __syncthreads();
-        break;
-      }
-      // drop kdrop, keeping the order of the remaining columns
-      {
-        const int k = kdrop;
-        const int idk = sW[k];
-        if (lane == (idk >> 2)) act &= ~(1u << (idk & 3));
-        __syncthreads();
-        for (int w = k; w < q - 1; ++w) {
-          if (lane < M) sB[w * M + lane] = sB[(w + 1) * M + lane];
-          if (lane == 0) {
-            su[w] = su[w + 1];
-            sW[w] = sW[w + 1];
+        // rotate d(q:) onto d(q), same rotations on J's columns (running value carried down)
+        double carry = sd[M - 1];
+#pragma unroll
+        for (int k = MAXM - 1; k >= 1; --k) {
+          if (k > q && k < M) {
+            const double a = sd[k - 1];
+            if (carry != 0.0) {
+              const double rho = sqrt(a * a + carry * carry);
+              const double ri = 1.0 / rho;
+              const double cs = a * ri, sn = carry * ri;
+              const double j0v = Jr[k - 1], j1v = Jr[k];
+              Jr[k - 1] = cs * j0v + sn * j1v;
+              Jr[k] = -sn * j0v + cs * j1v;
+              carry = rho;
+            } else {
+              carry = a;
+            }
           }
         }
-        --q;
-        __syncthreads();
+        // new column q of R_A = [d(0:q-1); carry]
+        if (lane < q) sRA[lane * M + q] = dk;
+        if (lane == q) {
+          sRA[q * M + q] = carry;
+          su[q] = upm;
+          sW[q] = p;
+        }
+        if (lane == mp) act |= 1u << kindp;
+        ++q;
+        lds_sync();
+        PSTAMP(PROF_QADD);
+        break;
       }
+      // ---- drop constraint kdrop: remove its column of R_A, re-triangularise with Givens
+      const int kd = kdrop;
+      lds_sync();
+      const int idk = sW[kd];
+      if (lane == (idk >> 2)) act &= ~(1u << (idk & 3));
+      if (lane < q) {  // shift columns kd+1..q-1 left (lanes = rows)
+        for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
+      }
+      if (lane == 0) {
+        for (int w = kd; w < q - 1; ++w) {
+          su[w] = su[w + 1];
+          sW[w] = sW[w + 1];
+        }
+      }
+      lds_sync();
+#pragma unroll
+      for (int jj = 0; jj < MAXM - 1; ++jj) {
+        if (jj >= kd && jj < q - 1) {
+          const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
+          if (b != 0.0) {
+            const double rho = sqrt(a * a + b * b);
+            const double ri = 1.0 / rho;
+            const double cs = a * ri, sn = b * ri;
+            if (lane >= jj && lane < q - 1) {  // rows jj, jj+1 of R_A (lanes = columns)
+              const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
+              sRA[jj * M + lane] = cs * r0 + sn * r1;
+              sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
+            }
+            const double j0v = Jr[jj], j1v = Jr[jj + 1];
+            Jr[jj] = cs * j0v + sn * j1v;
+            Jr[jj + 1] = -sn * j0v + cs * j1v;
+          }
+          lds_sync();
+        }
+      }
+      --q;
+      PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;
         break;
       }
     }
-    if (it >= maxit) break;
+    if (it >= maxit || infeas) break;
   }
-  __syncthreads();
+  lds_sync();
   return it;
 }
 
+
 template <int MAXM>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
                            const double* __restrict__ deltav, const double* __restrict__ lambdav,
@@ -345,6 +423,10 @@ __global__ void __launch_bounds__(64)
   const int N2 = N2v[c], Nu = Nuv[c];
   const int M = nu * Nu;
   int st = 0;
+#ifdef MPCT_PROFILE
+  unsigned long long pacc[PROF_N] = {};
+  unsigned long long pprev = __builtin_amdgcn_s_memtime();
+#endif
 
   auto write_nan = [&](int status) {
     if (lane < my) {
@@ -366,229 +448,293 @@ __global__ void __launch_bounds__(64)
     write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
-  const LdsLayout L = lds_layout(M, nx, nu, nin, ne, my, sc.tlen);
-  double* sH = lds + L.hinv;
+  const LdsLayout L = lds_layout(M, nx, nu, nin, ne, my, sc.tlen, sc.pl_maxb, sc.pl_maxa);
+  double* sRi = lds + L.rinv;
   double* sA = lds + L.A;
   double* sx = lds + L.x;
   double* sxc = lds + L.xc;
   double* suprev = lds + L.uprev;
+  double* syprev = lds + L.yprev;
   double* sucum = lds + L.ucum;
   double* sye = lds + L.ye;
   double* syeh = lds + L.yeh;
   double* sur = lds + L.uring;
+  double* splb = lds + L.plb;
+  double* spla = lds + L.pla;
   double* sstep = lds + L.step;
-  double* syprev = lds + L.yprev;  // raw y(t-1) per output
 
   // ------------------------------------------------------------------ prologue
   for (int e = lane; e < my * nu * sc.tlen; e += kWave) sstep[e] = sc.step[e];
-  for (int e = lane; e < L.Y - L.x; e += kWave) lds[L.x + e] = 0.0;  // persistent state
-  __syncthreads();
+  for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
+  for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
+  for (int e = lane; e < L.plb - L.x; e += kWave) lds[L.x + e] = 0.0;  // state + histories
+  // per-lane constants in registers
+  const int yoff_i = lane < my ? sc.yoff[lane] : 0;
+  const int nyh_i = lane < my ? sc.nyhi[lane] : 0;
+  const int upoff_n = lane < nu ? sc.upoff[lane] : 0;
+  const int dum_n = lane < nu ? sc.dum[lane] : 0;
+  RowCons rcn;
+  rcn.n = lane < M ? lane / Nu : 0;
+  rcn.l = lane < M ? lane - rcn.n * Nu : 0;
+  rcn.dmin = sc.bnd[rcn.n];
+  rcn.dmax = sc.bnd[nu + rcn.n];
+  rcn.umin = sc.bnd[2 * nu + rcn.n];
+  rcn.umax = sc.bnd[3 * nu + rcn.n];
+  const int ecopy = lane / ne;
+  const int ee = lane - ecopy * ne;
+  const int ej = ee % nin;
+  const int e_nb = (lane < ne * 2) ? sc.pl_nb[ee] : 0;
+  const int e_na = (lane < ne * 2) ? sc.pl_na[ee] : 0;
   const double* dl = deltav + c * my;
   const double* lm = lambdav + c * nu;
+  lds_sync();
 
-  // QR of the weighted least-squares matrix W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens
-  // rotations, carrying the right-hand block V = [Q^1/2 Phi_dev; 0]  (the
-  // normal equations G'QG + Lambda reach cond 1e12 on the config-2 grid and lose ~1e-5).
-  // Lane l owns column l of [R | T] (l < M: R, else T = Q1'V); rotation k is decided by lane k
-  // and broadcast with a wave shuffle.  The Lambda^1/2 rows are already triangular: R0 = Lambda^1/2.
+  // QR of W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens rotations carrying V = [Q^1/2 Phi; 0]
+  // (lane l owns column l of [R | T]; rotation k decided by lane k, broadcast with v_readlane).
   const int ncol = M + nx;  // <= 64 (checked on the host)
-  const int l = lane;
-  double rc[MAXM];
+  double rcol[MAXM];
   {
     double wl0 = 0.0;
-    if (l < M) {
-      const double ln = fabs(lm[l / Nu]);
+    if (lane < M) {
+      const double ln = fabs(lm[lane / Nu]);
       wl0 = sc.wsq ? ln : sqrt(ln);
     }
 #pragma unroll
-    for (int k = 0; k < MAXM; ++k) rc[k] = (k == l) ? wl0 : 0.0;
+    for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? wl0 : 0.0;
+  }
+  int gn = 0, gc = 0;
+  if (lane < M) {
+    gn = lane / Nu;
+    gc = lane - gn * Nu;
   }
   for (int i = 0; i < my; ++i) {
     const double di = fabs(dl[i]);
     const double sqi = sc.wsq ? di : sqrt(di);
     const int n1 = sc.n1[i];
-    const double* stp = sstep + i * nu * sc.tlen;
+    const double* stp = sstep + i * nu * sc.tlen + gn * sc.tlen;
+    const double* prow = sc.phi + (long long)(i * sc.n2max) * nx + (lane - M);
+    double wnext = 0.0;
+    if (lane < M) {
+      const int tt = n1 - gc;
+      wnext = tt >= 0 ? stp[tt] : 0.0;
+    } else if (lane < ncol) {
+      wnext = prow[0];
+    }
     for (int r = 0; r < N2; ++r) {
-      double w = 0.0;
-      if (l < M) {
-        const int n = l / Nu, cc = l - n * Nu, tt = n1 + r - cc;
-        w = tt >= 0 ? stp[n * sc.tlen + tt] : 0.0;
-      } else if (l < ncol) {
-        w = sc.phi[(long long)(i * sc.n2max + r) * nx + (l - M)];
+      double w = wnext * sqi;
+      if (r + 1 < N2) {  // prefetch the next row
+        if (lane < M) {
+          const int tt = n1 + r + 1 - gc;
+          wnext = tt >= 0 ? stp[tt] : 0.0;
+        } else if (lane < ncol) {
+          wnext = prow[(long long)(r + 1) * nx];
+        }
       }
-      w *= sqi;
 #pragma unroll
       for (int k = 0; k < MAXM; ++k) {
         if (k < M) {
-          const double b = __shfl(w, k, 64);
+          const double b = bcast(w, k);
           if (b != 0.0) {
-            const double a = __shfl(rc[k], k, 64);
-            const double rho = sqrt(a * a + b * b);
-            const double cs = a / rho, sn = b / rho;
-            const double rk = rc[k];
-            rc[k] = cs * rk + sn * w;
+            const double a = bcast(rcol[k], k);
+            const double rinv = 1.0 / sqrt(a * a + b * b);
+            const double cs = a * rinv, sn = b * rinv;
+            const double rk = rcol[k];
+            rcol[k] = cs * rk + sn * w;
             w = -sn * rk + cs * w;
           }
         }
       }
     }
   }
-  // R to LDS (row-major, upper); singular R -> non-finite status
-  if (l < M) {
+  // R (upper) to LDS scratch (row-major) in the step-table region; singular R -> status
+  double* sR = sstep;
+  lds_sync();
+  if (lane < M) {
 #pragma unroll
     for (int k = 0; k < MAXM; ++k)
-      if (k < M) sH[k * M + l] = rc[k];
+      if (k < M) sR[k * M + lane] = rcol[k];
   }
-  __syncthreads();
+  lds_sync();
   bool spd = true;
   for (int k = 0; k < M; ++k)
-    if (!(sH[k * M + k] > 0.0)) spd = false;
+    if (!(sR[k * M + k] > 0.0)) spd = false;
   if (!spd) {
     write_nan(MPCT_ST_NONFINITE_);
     return;
   }
-  // A = -R^-1 T (lanes M..M+nx-1, own column, back substitution), column-major [s][m]
-  if (l >= M && l < ncol) {
+  // A = -R^-1 T (lanes M..M+nx-1 solve for their own column), column-major [s][m]
+  if (lane >= M && lane < ncol) {
 #pragma unroll
     for (int kk = MAXM - 1; kk >= 0; --kk) {
       if (kk < M) {
-        double a = rc[kk];
+        double a = rcol[kk];
 #pragma unroll
         for (int j = 0; j < MAXM; ++j)
-          if (j > kk && j < M) a -= sH[kk * M + j] * rc[j];
-        rc[kk] = a / sH[kk * M + kk];
+          if (j > kk && j < M) a -= sR[kk * M + j] * rcol[j];
+        rcol[kk] = a / sR[kk * M + kk];
       }
     }
 #pragma unroll
     for (int m = 0; m < MAXM; ++m)
-      if (m < M) sA[(l - M) * M + m] = -rc[m];
+      if (m < M) sA[(lane - M) * M + m] = -rcol[m];
   }
-  // R^-1 (upper) for the active-set method: lane j solves R x = e_j
-  double* sRinv = lds + L.Y;  // temporary (union region; step table no longer needed)
-  if (l < M) {
-    double x[MAXM];
+  // R^-1 (upper): lane j solves R x = e_j; stored row-major, row m also kept in registers
+  if (lane < M) {
+    double xr[MAXM];
 #pragma unroll
-    for (int kk = 0; kk < MAXM; ++kk) x[kk] = 0.0;
+    for (int kk = 0; kk < MAXM; ++kk) xr[kk] = 0.0;
 #pragma unroll
     for (int kk = MAXM - 1; kk >= 0; --kk) {
-      if (kk < M) {
-        double a = (kk == l) ? 1.0 : 0.0;
+      if (kk < M && kk <= lane) {
+        double a = (kk == lane) ? 1.0 : 0.0;
 #pragma unroll
         for (int j = 0; j < MAXM; ++j)
-          if (j > kk && j < M) a -= sH[kk * M + j] * x[j];
-        x[kk] = (kk <= l) ? a / sH[kk * M + kk] : 0.0;
+          if (j > kk && j < M) a -= sR[kk * M + j] * xr[j];
+        xr[kk] = a / sR[kk * M + kk];
       }
     }
 #pragma unroll
     for (int kk = 0; kk < MAXM; ++kk)
-      if (kk < M) sRinv[kk * M + l] = x[kk];
+      if (kk < M) sRi[kk * M + lane] = xr[kk];
   }
-  __syncthreads();
-  for (int e = lane; e < M * M; e += kWave) sH[e] = sRinv[e];
-  __syncthreads();
+  lds_sync();
+  PSTAMP(PROF_PROLOGUE);
+#ifdef MPCT_EXP_NOLOOP
+  if (lane == 0 && out.J1) out.J1[sim] = sA[lane] + sRi[lane];
+  return;
+#endif
 
-  const double* bnd = sc.bnd;
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 8 * M + 16;
   long long iters = 0;
   const double* rr = rv + (long long)kref * my * nit;
   const double* vvk = vv ? vv + (long long)kref * sc.nd * nit : nullptr;
 
-  // unconstrained minimiser dU = A * state, then the QP; result in sxc
+  // unconstrained minimiser dU = A x, then the QP; result in sxc
   auto solve_step = [&]() {
     if (lane < M) {
-      double a0 = 0.0, a1 = 0.0;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       int s = 0;
-      for (; s + 1 < nx; s += 2) {
+      for (; s + 3 < nx; s += 4) {
         a0 += sA[s * M + lane] * sx[s];
         a1 += sA[(s + 1) * M + lane] * sx[s + 1];
+        a2 += sA[(s + 2) * M + lane] * sx[s + 2];
+        a3 += sA[(s + 3) * M + lane] * sx[s + 3];
       }
-      if (s < nx) a0 += sA[s * M + lane] * sx[s];
-      sxc[lane] = a0 + a1;
+      for (; s < nx; ++s) a0 += sA[s * M + lane] * sx[s];
+      sxc[lane] = (a0 + a1) + (a2 + a3);
     }
-    __syncthreads();
-    iters += gi_qp<MAXM>(lds, L, M, Nu, nu, bnd, tol, maxit, &st);
+    lds_sync();
+    PSTAMP(PROF_UNC);
+#ifndef MPCT_EXP_NOQP
+    iters += gi_qp<MAXM>(lds, L, M, rcn, tol, maxit, &st
+#ifdef MPCT_PROFILE
+                         , pacc, pprev
+#endif
+    );
+#endif
+    PSTAMP(PROF_QP);
   };
 
   // ------------------------------------------------------------------ open-loop prediction
   double jnu = 0.0;
   if (o.open_loop) {
     // closedloop_toolbox.m:86-91: initial state (y = 0), reference r(:, end)
-    if (lane < my) sx[sc.yoff[lane]] = -rr[lane * nit + (nit - 1)];
-    __syncthreads();
+    if (lane < my) sx[yoff_i] = -rr[lane * nit + (nit - 1)];
+    lds_sync();
     solve_step();
     if (lane < M) {
-      int n = lane / Nu, l = lane - n * Nu;
       double s = 0.0;
-      for (int j = n * Nu; j <= n * Nu + l; ++j) s += sxc[j];
+      for (int j = lane - rcn.l; j <= lane; ++j) s += sxc[j];
       sucum[lane] = s;  // Uopt row l for MV n (held after Nu-1)
     }
-    __syncthreads();
+    lds_sync();
     if (lane < nu) {
       // VNS2.m:183-191: Xnu = |uopt(:,1)| ./ |diff(uopt)|, inf/NaN -> 0, Jnu = sum Xnu^2
-      double u0 = fabs(sucum[lane * Nu]);
-      int nd_ = Nu - 1 < nit - 1 ? Nu - 1 : nit - 1;
+      const double u0 = fabs(sucum[lane * Nu]);
+      const int nd_ = Nu - 1 < nit - 1 ? Nu - 1 : nit - 1;
       for (int t = 0; t < nd_; ++t) {
-        double dd = fabs(sucum[lane * Nu + t + 1] - sucum[lane * Nu + t]);
-        double xr = u0 / dd;
+        const double dd = fabs(sucum[lane * Nu + t + 1] - sucum[lane * Nu + t]);
+        const double xr = u0 / dd;
         if (isfinite(xr)) jnu += xr * xr;
       }
     }
-    if (lane < my) sx[sc.yoff[lane]] = 0.0;
-    __syncthreads();
+    if (lane < my) sx[yoff_i] = 0.0;
+    lds_sync();
+    PSTAMP(PROF_OPENLOOP);
   }
 
   // ------------------------------------------------------------------ closed loop
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
   const int ncopy = o.open_loop ? 2 : 1;
+  const bool is_entry = lane < ncopy * ne;
+  const double* eb = splb + ee * sc.pl_maxb;
+  const double* ea = spla + ee * sc.pl_maxa;
+  double* eyh = syeh + lane * kYeHist;
+  const double* eur = sur + (ecopy * nin + ej) * kURing;
+  // prefetched per-output signals
+  double r_t = 0.0, yr_t = 0.0;
+  if (lane < my) {
+    r_t = rr[lane * nit];
+    yr_t = sc.yref[lane * nit];
+  }
   for (int t = 0; t < nit; ++t) {
+    double r_n = 0.0, yr_n = 0.0;
+    if (lane < my && t + 1 < nit) {  // prefetch t+1
+      r_n = rr[lane * nit + t + 1];
+      yr_n = sc.yref[lane * nit + t + 1];
+    }
     // inputs at time t that are already known: MDs v(t); open-loop uopt(t)
     if (sc.nd > 0) {
       for (int e = lane; e < ncopy * sc.nd; e += kWave) {
-        int cpy = e / sc.nd, j = e - cpy * sc.nd;
+        const int cpy = e / sc.nd, j = e - cpy * sc.nd;
         sur[(cpy * nin + nu + j) * kURing + (t & (kURing - 1))] = vvk[j * nit + t];
       }
     }
     if (o.open_loop && lane < nu) {
-      int l = t < Nu - 1 ? t : Nu - 1;
+      const int l = t < Nu - 1 ? t : Nu - 1;
       sur[(nin + lane) * kURing + (t & (kURing - 1))] = sucum[lane * Nu + l];
     }
-    __syncthreads();
+    lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    for (int e = lane; e < ncopy * ne; e += kWave) {
-      const int cpy = e / ne, ee = e - cpy * ne, j = ee % nin;
-      const double* b = sc.pl_b + ee * sc.pl_maxb;
-      const double* a = sc.pl_a + ee * sc.pl_maxa;
-      const double* ur = sur + (cpy * nin + j) * kURing;
-      double* yh = syeh + e * kYeHist;
-      double acc = 0.0;
-      const int nb = sc.pl_nb[ee], na = sc.pl_na[ee];
-      for (int l = 0; l < nb; ++l)
-        if (t - l >= 0) acc += b[l] * ur[(t - l) & (kURing - 1)];
-      for (int l = 1; l < na; ++l)
-        if (t - l >= 0) acc -= a[l] * yh[(t - l) & (kYeHist - 1)];
-      yh[t & (kYeHist - 1)] = acc;
-      sye[e] = acc;
+    if (is_entry) {
+      // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int l = 0; l < kMaxTaps; l += 2) {
+        if (l < e_nb) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
+        if (l + 1 < e_nb) a1 += eb[l + 1] * eur[(t - l - 1) & (kURing - 1)];
+      }
+#pragma unroll
+      for (int l = 1; l < kYeHist; ++l)
+        if (l < e_na) a0 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
+      const double acc = a0 + a1;
+      eyh[t & (kYeHist - 1)] = acc;
+      sye[lane] = acc;
     }
-    __syncthreads();
+    lds_sync();
+    PSTAMP(PROF_PLANT);
     if (lane < my) {
       const int i = lane;
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
-      const int yo = sc.yoff[i], nh = sc.nyhi[i];
+      double hist[kYeHist];
+#pragma unroll
+      for (int k = 1; k < kYeHist; ++k) hist[k] = k < nyh_i ? sx[yoff_i + k] : 0.0;
       double cur = y, prev = syprev[i];
-      for (int k = 1; k < nh; ++k) {
-        const double old = sx[yo + k];
-        const double nk = cur - prev;
-        sx[yo + k] = nk;
-        cur = nk;
-        prev = old;
+#pragma unroll
+      for (int k = 1; k < kYeHist; ++k) {
+        if (k < nyh_i) {
+          const double nk = cur - prev;
+          sx[yoff_i + k] = nk;
+          cur = nk;
+          prev = hist[k];
+        }
       }
       syprev[i] = y;
-      sx[yo] = y - rr[i * nit + t];
-      const double yr = sc.yref[i * nit + t];
-      const double e1 = y - yr;
+      sx[yoff_i] = y - r_t;
+      const double e1 = y - yr_t;
       j1 += e1 * e1;
       if (t >= sc.ink0) j22 += e1 * e1;
       double ysv = 0.0;
@@ -601,28 +747,40 @@ __global__ void __launch_bounds__(64)
         if (o.open_loop && out.ys) out.ys[(sim * my + i) * nit + t] = ysv;
       }
     }
-    __syncthreads();
+    lds_sync();
+    PSTAMP(PROF_YUPD);
     solve_step();
     if (lane < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
-      const int uo = sc.upoff[n], nh = sc.dum[n];
-      for (int k = nh - 1; k > 0; --k) sx[uo + k] = sx[uo + k - 1];
-      sx[uo] = du;
+      double h[kMaxDum];
+#pragma unroll
+      for (int k = 0; k < kMaxDum - 1; ++k) h[k] = k < dum_n - 1 ? sx[upoff_n + k] : 0.0;
+#pragma unroll
+      for (int k = 1; k < kMaxDum; ++k)
+        if (k < dum_n) sx[upoff_n + k] = h[k - 1];
+      sx[upoff_n] = du;
       sur[n * kURing + (t & (kURing - 1))] = un;
       if (o.want_traj) {
         if (out.u) out.u[(sim * nu + n) * nit + t] = un;
         if (o.open_loop && out.uopt) {
-          int l = t < Nu - 1 ? t : Nu - 1;
+          const int l = t < Nu - 1 ? t : Nu - 1;
           // Info.Uopt has p+1 rows then the padding repeats the last row (:94-98)
           out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
         }
       }
       suprev[n] = un;
     }
-    __syncthreads();
+    lds_sync();
+    r_t = r_n;
+    yr_t = yr_n;
+    PSTAMP(PROF_UUPD);
   }
+#ifdef MPCT_PROFILE
+  if (lane == 0 && out.prof)
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+#endif
 
   // ------------------------------------------------------------------ results
   if (lane < my) {
@@ -632,9 +790,9 @@ __global__ void __launch_bounds__(64)
     if (out.j21) out.j21[sim * my + lane] = o.open_loop ? j21 : NAN;
   }
   if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = o.open_loop ? jnu : NAN;
-  unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
+  const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
   if (lane == 0) {
-    int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
+    const int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
     if (out.status) out.status[sim] = s;
     if (out.qp_iters) out.qp_iters[sim] = iters;
   }
@@ -646,12 +804,15 @@ __global__ void __launch_bounds__(64)
 // host-side launch
 #include <string>
 
+#ifndef MPCT_WAVES_PER_EU
+#define MPCT_WAVES_PER_EU 1
+#endif
 namespace mpct {
 
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {
   (void)N2;
   const int M = sc.nu * Nu;
-  LdsLayout L = lds_layout(M, sc.nx, sc.nu, sc.nin, sc.ne, sc.my, sc.tlen);
+  LdsLayout L = lds_layout(M, sc.nx, sc.nu, sc.nin, sc.ne, sc.my, sc.tlen, sc.pl_maxb, sc.pl_maxa);
   return (long long)L.total * 8;
 }
 

@@ -7,8 +7,10 @@ namespace mpct {
 
 constexpr int kMaxOut = 16;    // outputs (my)
 constexpr int kMaxIn = 16;     // inputs (nu + nd)
-constexpr int kURing = 64;     // plant input history ring (power of two)
+constexpr int kURing = 32;     // plant input history ring (power of two)
+constexpr int kMaxTaps = 16;   // longest plant numerator incl. delay (z^-1 taps)
 constexpr int kYeHist = 8;     // plant entry output history ring (power of two)
+constexpr int kMaxDum = 16;    // longest past-control register per MV (deltaUFree cp)
 constexpr int kWave = 64;
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
@@ -53,6 +55,11 @@ struct DevResult {
   int32_t* status;
   int64_t* qp_iters;
   double *y, *u, *ys, *uopt;
+  unsigned long long* prof;  // diagnostic builds only (-DMPCT_PROFILE): [sim][8] cycle sums
 };
+
+// section ids of the diagnostic in-kernel stamps
+enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,
+       PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_N = 12 };
 
 }  // namespace mpct

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <cstdio>
 
 #include "../../include/mpct.h"
 #include "mpct_dev.h"
@@ -282,7 +283,17 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       return fail(MPCT_EINVAL, "plant has direct feedthrough from an MV (algebraic loop)");
     }
   }
-  if (s->pl_maxb > kURing || s->pl_maxa > kYeHist) {
+  for (int n = 0; n < nu; ++n)
+    if (s->dum[n] > kMaxDum) {
+      delete s;
+      return fail(MPCT_ERANGE, "past-control register longer than the device supports (16)");
+    }
+  for (int i = 0; i < my; ++i)
+    if (s->nyhi[i] > kYeHist) {
+      delete s;
+      return fail(MPCT_ERANGE, "CARIMA denominator order too high for the device (na <= 7)");
+    }
+  if (s->pl_maxb > kMaxTaps || s->pl_maxa > kYeHist) {
     delete s;
     return fail(MPCT_ERANGE, "plant entry too long for the device history rings");
   }
@@ -460,11 +471,37 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   if (C == 0) return MPCT_OK;
   DevOpts dop = make_opts(opts);
   DevResult dr{out->J1, out->j21, out->j22, out->Jnu, out->status, out->qp_iters,
-                out->y, out->u, out->ys, out->uopt};
+                out->y, out->u, out->ys, out->uopt, nullptr};
+#ifdef MPCT_PROFILE
+  // diagnostic build: per-simulation section cycle sums, summarised on stderr
+  const long long S = C * nref;
+  unsigned long long* dprof = nullptr;
+  (void)hipMalloc(&dprof, sizeof(unsigned long long) * S * PROF_N);
+  dr.prof = dprof;
+#endif
   std::string err;
   rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
                           static_cast<hipStream_t>(stream), &err);
   if (rc) return fail(rc, err);
+#ifdef MPCT_PROFILE
+  {
+    std::vector<unsigned long long> hp(S * PROF_N);
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    (void)hipMemcpy(hp.data(), dprof, sizeof(unsigned long long) * S * PROF_N, hipMemcpyDeviceToHost);
+    (void)hipFree(dprof);
+    double sum[PROF_N] = {0}, mx[PROF_N] = {0};
+    for (long long i = 0; i < S; ++i)
+      for (int k = 0; k < PROF_N; ++k) {
+        sum[k] += (double)hp[i * PROF_N + k];
+        mx[k] = std::max(mx[k], (double)hp[i * PROF_N + k]);
+      }
+    const char* nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
+                              "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop"};
+    fprintf(stderr, "[mpct profile] mean / max cycles per simulation over %lld sims\n", S);
+    for (int k = 0; k < PROF_N; ++k)
+      fprintf(stderr, "  %-14s %12.0f %12.0f\n", nm[k], sum[k] / (double)S, mx[k]);
+  }
+#endif
   return MPCT_OK;
 }
 
@@ -556,5 +593,7 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.nx = s->nx;
   ds.ne = s->ne;
   ds.tlen = s->tlen;
+  ds.pl_maxb = s->pl_maxb;
+  ds.pl_maxa = s->pl_maxa;
   return lds_bytes_for(ds, N2, Nu);
 }

@@ -66,6 +66,9 @@ _lib = None
 
 
 def lib_path() -> str:
+    override = os.environ.get("MPCT_LIB")  # e.g. the -DMPCT_PROFILE diagnostic build
+    if override:
+        return override
     for p in _CANDIDATES:
         if os.path.exists(p):
             return p
