@@ -1,0 +1,57 @@
+"""Candidate-level data parallelism: one process per GPU, contiguous candidate
+shards, one all-gather of the per-candidate cost records, identical ranking on every rank.
+
+Nothing is exchanged during a simulation (VNS2.m:148-169 and GAM_fun.m:79-91 evaluate every
+candidate in isolation), so the only collective is the final all-gather.  The functions here are
+backend-agnostic (torch.distributed with "nccl" = RCCL on the GPU box, "gloo" in the CPU tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+SKIPPED_N2 = 0  # sentinel candidate: the kernel returns status MPCT_ST_SKIPPED (8) and NaN costs
+
+
+def shard_range(C: int, world: int, rank: int):
+    """[lo, hi) of rank's contiguous shard of a C-candidate grid padded to a multiple of world
+    (per = ceil(C / world)); hi may exceed C — those slots are sentinel padding."""
+    per = -(-C // world)
+    return rank * per, (rank + 1) * per
+
+
+def pad_shard(N2, Nu, delta, lam, lo: int, hi: int):
+    """Slice [lo, hi) of the candidate arrays, padding past the end with skipped sentinels."""
+    C = len(N2)
+    n = hi - lo
+    take = max(0, min(hi, C) - lo)
+    my, nu = delta.shape[1], lam.shape[1]
+    oN2 = np.full(n, SKIPPED_N2, dtype=np.int32)
+    oNu = np.ones(n, dtype=np.int32)
+    od = np.ones((n, my))
+    ol = np.ones((n, nu))
+    oN2[:take], oNu[:take] = N2[lo:lo + take], Nu[lo:lo + take]
+    od[:take], ol[:take] = delta[lo:lo + take], lam[lo:lo + take]
+    return oN2, oNu, od, ol
+
+
+def gather_costs(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather equal-size per-rank cost records [n, K] -> [world * n, K] in rank order."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    return out
+
+
+def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = None) -> torch.Tensor:
+    """Candidate order by ascending weighted cost (Shell3x3.m:161 Pareto weights), ties by
+    candidate index; NaN costs (failed / sentinel candidates) sort last.  Identical on every
+    rank because every rank sorts the same gathered tensor."""
+    s = costs @ weights
+    if C is not None:
+        s = s[:C]
+    s = torch.where(torch.isnan(s), torch.full_like(s, float("inf")), s)
+    return torch.argsort(s, stable=True)

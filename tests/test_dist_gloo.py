@@ -1,0 +1,92 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py — contiguous
+candidate shards with sentinel padding, one all-gather of the per-candidate cost records, and an
+identical ranking on every rank that equals the single-process ranking.  Per-candidate costs come
+from the C port (oracle/cgpc.c) here, standing in for the kernel, which needs a GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _costs(N2, Nu, d, l):
+    """Cost records [n, my] for a shard; sentinel candidates (N2 == 0) -> NaN like the kernel."""
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3
+
+    osc, r, yref, _ = shell3x3()
+    out = np.full((len(N2), 3), np.nan)
+    ok = N2 > 0
+    if ok.any():
+        res = CPort(osc, 30, 500, yref).eval(N2[ok], Nu[ok], d[ok], l[ok], r[None], threads=1)
+        out[ok] = res["J1"]
+    return out
+
+
+def _worker(rank, world, port, C, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_range
+        from mpct.scenarios import candidate_grid
+
+        N2, Nu, d, l = candidate_grid(C)
+        lo, hi = shard_range(C, world, rank)
+        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, lo, hi)
+        local = torch.from_numpy(_costs(sN2, sNu, sd, sl))
+        g = gather_costs(local)
+        w = torch.tensor([0.05, 0.40, 0.55], dtype=torch.float64)
+        order = rank_candidates(g, w, C)
+        q.put((rank, g.numpy(), order.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("C", [12, 11])
+def test_two_rank_gather_and_rank(built, C):
+    from mpct.scenarios import candidate_grid
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got.sort(key=lambda t: t[0])
+    N2, Nu, d, l = candidate_grid(C)
+    ref = _costs(N2, Nu, d, l)
+    w = np.array([0.05, 0.40, 0.55])
+    ref_order = np.argsort(ref @ w, kind="stable")
+    per = -(-C // world)
+    for rank, g, order in got:
+        assert g.shape == (world * per, 3)
+        np.testing.assert_array_equal(g[:C], ref)              # bit-identical gathered records
+        assert np.all(np.isnan(g[C:]))                         # sentinel padding
+        np.testing.assert_array_equal(order, ref_order)        # identical ranking on every rank
+    np.testing.assert_array_equal(got[0][2], got[1][2])
+
+
+def test_shard_range_covers_grid():
+    from mpct.dist import shard_range
+
+    for C in (1, 7, 4096, 65536):
+        for W in (1, 2, 3, 8):
+            spans = [shard_range(C, W, r) for r in range(W)]
+            assert spans[0][0] == 0 and all(spans[i][1] == spans[i + 1][0] for i in range(W - 1))
+            assert spans[-1][1] >= C and spans[-1][1] - C < W
