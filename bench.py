@@ -133,6 +133,17 @@ def main():
     fl = algorithmic_flops_per_sim(sc, args.n2, args.nu, I_as) * C
     achieved = fl / (kms * 1e-3) / 1e12
 
+    # PCIe-inclusive rate of the host-buffer entry point (mpct_eval_batch: H2D candidates,
+    # kernel, D2H costs), after the timed region; reported beside `value`, never as `value`
+    from mpct.engine import eval_batch
+
+    hN2, hNu, hd, hl = sN2, sNu, sd, sl
+    eval_batch(sc, hN2, hNu, hd, hl, r[None], device=local)
+    t2 = time.perf_counter()
+    for _ in range(3):
+        eval_batch(sc, hN2, hNu, hd, hl, r[None], device=local)
+    host_rate = 3 * C / (time.perf_counter() - t2)
+
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -200,6 +211,7 @@ def main():
                      "kernel": "gpc_closed_loop_kernel", "kernel_ms": kms,
                      "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as},
         "cpu_baseline": cpu,
+        "host_api_sims_per_s": host_rate,
         "status_nonzero": nbad,
         "top_candidate": int(order[0].item()),
     }

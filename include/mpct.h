@@ -16,7 +16,7 @@
  *   - negative return codes are argument / shape / device errors (message in
  *     mpct_last_error(), thread-local); per-candidate numerical trouble never fails the call:
  *     it is reported in mpct_result.status[] with NaN costs (the reference swallows such
- *     errors with fprintf and continues: VNS2.m:161-163, GAM_fun.m:191-193).
+ *     errors with fprintf and continues: VNS2.m:161-163, GAM_fun.m:82-84).
  *   - threading: one scenario per host thread, or external synchronisation.  All device work
  *     of a call is complete when mpct_eval_batch returns.
  */
@@ -48,7 +48,7 @@ extern "C" {
 
 /* One SISO discrete transfer function  y = z^-delay * num(z)/den(z) u  in the form tfdata(.,'v')
  * returns it (descending powers of z, numerator padded to the denominator's length, den[0]=1)
- * — the representation descompMPC.m:194 reads.  len = number of coefficients of each. */
+ * — the representation descompMPC.m:19 reads.  len = number of coefficients of each. */
 typedef struct mpct_dtf {
   int32_t len;
   const double* num;
@@ -112,7 +112,7 @@ typedef struct mpct_opts {
 /* Results, one row per SIMULATION s = c*nref + k (candidate c, reference k).  Any pointer may
  * be NULL to skip that output.  Sizes: J1/j21/j22 [S*my], Jnu [S*nu], status/qp_iters [S],
  * y/ys [S*my*nit], u/uopt [S*nu*nit].
- *   J1[i]  = sum_t (y_i - yref_i)^2                       GAM_fun.m:219-220
+ *   J1[i]  = sum_t (y_i - yref_i)^2                       GAM_fun.m:110-111
  *   j21[i] = sum_{t>=inK} (y_i - ys_i)^2                   VNS2.m:172,176
  *   j22[i] = sum_{t>=inK} (y_i - yref_i)^2                 VNS2.m:173,177
  *   Jnu[n] = sum_t (|uopt_n(1)| / |diff(uopt_n)|)^2, inf/NaN -> 0   VNS2.m:183-191           */

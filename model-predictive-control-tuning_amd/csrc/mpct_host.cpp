@@ -164,7 +164,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     o += d->na[i] + 1;
   }
   s->nyh = o;
-  // cp(i,n) = dp + length(B) - 1  (deltaUFree.m:288-292)
+  // cp(i,n) = dp + length(B) - 1  (deltaUFree.m:25-29)
   std::vector<int> cp(my * nu);
   s->dum.assign(nu, 0);
   for (int i = 0; i < my; ++i)
@@ -224,10 +224,10 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
         std::vector<double> aux = conv(E, B);
         std::vector<double> BE;
         for (double v : aux)
-          if (v != 0.0) BE.push_back(v);  // deltaUFree.m:302-308: every zero removed
+          if (v != 0.0) BE.push_back(v);  // deltaUFree.m:40-45: every zero removed
         const int c = cp[i * nu + n];
         const int lBE = (int)BE.size();
-        double* dst = prow + s->upoff[n];  // left-aligned block (cell2mat2.m:275)
+        double* dst = prow + s->upoff[n];  // left-aligned block (cell2mat2.m:56)
         if (lBE < c) {
           for (int k = 0; k < c - lBE; ++k) dst[k] = 0.0;
           for (int k = 0; k < lBE; ++k) dst[c - lBE + k] = BE[k];

@@ -15,7 +15,7 @@
  *   dU = argmin 1/2 dU'H dU + g'dU s.t. rate/amplitude bounds: unconstrained minimiser, then
  *        a Goldfarb-Idnani dual active-set method (same family as the toolbox's KWIK solver)
  *   u(t) = u(t-1) + dU(first move of every MV)
- * Costs: J1 (GAM_fun.m:219-220), j22 from inK (VNS2.m:173,177); open loop (uopt, ys, j21, Jnu)
+ * Costs: J1 (GAM_fun.m:110-111), j22 from inK (VNS2.m:173,177); open loop (uopt, ys, j21, Jnu)
  * restated as in closedloop_toolbox.m:85-100 / VNS2.m:172-191.
  *
  * Build: see oracle/Makefile (gcc -O3 -fopenmp -shared -fPIC).

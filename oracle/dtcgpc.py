@@ -45,8 +45,8 @@ def ba_mimo(Bn, An, round_roots: bool = True):
     numerators.
 
     round_roots=True is the reference verbatim: LCM poles are ``unique(round(roots(prod),4))``
-    (BA_MIMO.m:141-143) and B{i,j} = Bn{i,j} * poly(LCM roots not in round(roots(An{i,j}),4))
-    (BA_MIMO.m:151-163), including its index-skipping removal loop.  This perturbs the model by
+    (BA_MIMO.m:38-40) and B{i,j} = Bn{i,j} * poly(LCM roots not in round(roots(An{i,j}),4))
+    (BA_MIMO.m:48-60), including its index-skipping removal loop.  This perturbs the model by
     ~1e-5 (a deliberate model change in the reference).
 
     round_roots=False is the exact-model variant used for toolbox-equivalent semantics
@@ -59,7 +59,7 @@ def ba_mimo(Bn, An, round_roots: bool = True):
     Bn = [[np.array(Bn[i][j], dtype=float) for j in range(m)] for i in range(p)]
     for i in range(p):
         for j in range(m):
-            if Bn[i][j][0] == 0:  # BA_MIMO.m:125-127 strip ONE leading zero
+            if Bn[i][j][0] == 0:  # BA_MIMO.m:21-23 strip ONE leading zero
                 Bn[i][j] = Bn[i][j][1:]
     A = [None] * p
     B = [[None] * m for _ in range(p)]
@@ -177,7 +177,7 @@ def mat_g(P, N, Nu, d):
 # ---------------------------------------------------------------------------------------------
 def delta_u_free(B, En, N, dp):
     """deltaUFree.m:13-62.  uG{m,n}(i,:) = last cp coefficients of conv(En{m}(i,:), B{m,n})
-    after removing ALL zero coefficients (deltaUFree.m:302-308: the loop keeps aux(j) ~= 0 for
+    after removing ALL zero coefficients (deltaUFree.m:40-45: the loop keeps aux(j) ~= 0 for
     every j, not only trailing ones), cp = dp(m,n) + length(B{m,n}) - 1, left-padded with zeros
     when shorter.  Column order: Delta u(t-1), Delta u(t-2), ..., Delta u(t-cp)."""
     ny = len(B)

@@ -3,7 +3,7 @@
 Every function names the reference call sites it stands in for.  Discrete transfer functions
 are represented as :class:`DTF` (one SISO entry: z-domain ``num``/``den`` exactly as ``tfdata``
 returns them, plus the integer ``iodelay``), which is the representation the reference's
-``descompMPC.m:194`` reads.
+``descompMPC.m:19`` reads.
 """
 from __future__ import annotations
 
@@ -49,7 +49,7 @@ class DTF:
 
 
 # ---------------------------------------------------------------------------------------------
-# round(x, 4) — MATLAB rounds half away from zero (used at BA_MIMO.m:141,151-152)
+# round(x, 4) — MATLAB rounds half away from zero (used at BA_MIMO.m:38,48-49)
 # ---------------------------------------------------------------------------------------------
 def mround(x, n: int = 4):
     x = np.asarray(x)
@@ -60,14 +60,14 @@ def mround(x, n: int = 4):
 
 
 def conv(a, b):
-    """MATLAB conv (full) — DTC-GPC/diophantine.m:35, deltaUFree.m:298, BA_MIMO.m:135,163."""
+    """MATLAB conv (full) — DTC-GPC/diophantine.m:35, deltaUFree.m:35, BA_MIMO.m:32,60."""
     return np.convolve(np.asarray(a, dtype=float), np.asarray(b, dtype=float))
 
 
 def roots(c):
     """MATLAB roots (roots.m): strip leading zeros, turn trailing zeros into roots at the
     origin, and take the eigenvalues of the companion matrix of what is left.  Stands in for
-    BA_MIMO.m:141,151-152 and filtro_siso.m:131 (pole)."""
+    BA_MIMO.m:38,48-49 and filtro_siso.m:26 (pole)."""
     c = np.asarray(c, dtype=float).ravel()
     nz = np.nonzero(c)[0]
     if nz.size == 0:
@@ -107,7 +107,7 @@ def de2bi(x: int, n: int):
 
 # ---------------------------------------------------------------------------------------------
 # c2d(sys, Ts, 'zoh') for a continuous SISO tf with an input/output delay
-# (Shell3x3.m:65, Shell7x5.m:101, WoodBerry.m:57, DTC_GPC_WW.m:41, Shell3x3.m:77 Pref)
+# (Shell3x3.m:65, Shell7x5.m:95, WoodBerry.m:62, DTC_GPC_WW.m:41, Shell3x3.m:77 Pref)
 # ---------------------------------------------------------------------------------------------
 def _tf2ss(num, den):
     """Controllable canonical realisation of a strictly proper num/den (descending powers)."""
@@ -194,7 +194,7 @@ def c2d_fopdt(K: float, tau: float, Ts: float, delay: float) -> DTF:
 
 
 # ---------------------------------------------------------------------------------------------
-# Discrete simulation: step / lsim (MatG.m:239, OptimalPredictor2.m:28-37, closedloop_toolbox.m:100)
+# Discrete simulation: step / lsim (MatG.m:51, OptimalPredictor2.m:28-37, closedloop_toolbox.m:100)
 # ---------------------------------------------------------------------------------------------
 def lsim_dtf(sys: DTF, u) -> np.ndarray:
     """Full-history discrete simulation from rest (lsim of a discrete tf): direct form
