@@ -203,19 +203,61 @@ __device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m
 #endif
 
 // ------------------------------------------------------------------------------------------
-// Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
-// family) in its factored, numerically stable form.  H = R'R;
-// J (M x M) with H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].
-// For the most violated constraint p:  d = J'n_p,  z = J(:,q:) d(q:) (primal direction),
-// r = R_A^-1 d(0:q) (dual direction), beta = n_p'z = |d(q:)|^2.  Adding p rotates d(q:) onto
-// d(q) (Givens, applied to J's columns) and appends d(0:q) to R_A; dropping constraint k
-// re-triangularises R_A with Givens rotations applied to J's columns.
-// Lanes = rows of J (registers); d is distributed (lane k holds d_k) through one LDS dump of
-// the rows in the normal's support; R_A lives in LDS.  Starts from the unconstrained minimiser
-// in sxc.  Wave-uniform control flow.
+// lane shifts by one within the QP rows: DPP row_shl/row_shr when the rows fit one DPP row
 template <int MAXM>
-__device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const RowCons& rc,
-                     double tol, int maxit, int* st
+__device__ __forceinline__ double lane_next(double v) {  // lane i receives lane i+1
+  if constexpr (MAXM <= 16) return dppd<0x101>(v);
+  else return __shfl_down(v, 1, 64);
+}
+template <int MAXM>
+__device__ __forceinline__ double lane_prev(double v) {  // lane i receives lane i-1
+  if constexpr (MAXM <= 16) return dppd<0x111>(v);
+  else return __shfl_up(v, 1, 64);
+}
+template <int MAXM>
+__device__ __forceinline__ int lane_next_i(int v) {
+  if constexpr (MAXM <= 16) return dppi<0x101>(v);
+  else return __shfl_down(v, 1, 64);
+}
+
+// inclusive prefix sum of x over the lanes of one MV block (lane position l within its block):
+// the amplitude rows of the QP.  DPP row_shr Hillis-Steele scan when the rows fit one DPP row.
+template <int MAXM>
+__device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row, double* sxc) {
+  if constexpr (MAXM <= 16) {
+    double pre = x, t;
+    if (Nu > 1) { t = dppd<0x111>(pre); if (l >= 1) pre += t; }
+    if (Nu > 2) { t = dppd<0x112>(pre); if (l >= 2) pre += t; }
+    if (Nu > 4) { t = dppd<0x114>(pre); if (l >= 4) pre += t; }
+    if (Nu > 8) { t = dppd<0x118>(pre); if (l >= 8) pre += t; }
+    return pre;
+  } else {
+    const int lane = threadIdx.x;  // sxc holds the M QP rows only
+    if (row) sxc[lane] = x;
+    lds_sync();
+    double pre = 0.0;
+    if (row)
+      for (int j = lane - l; j <= lane; ++j) pre += sxc[j];
+    lds_sync();
+    return pre;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
+// family) in its factored, numerically stable form.  H = R'R;  J (M x M) with
+// H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].
+// For the most violated constraint p:  d = J'n_p,  z = J(:,q:) d(q:) (primal direction),
+// r = R_A^-1 d(0:q) (dual direction), beta = n_p'z = |d(q:)|^2.  Adding p applies ONE
+// Householder reflector to J(:,q:) mapping d(q:) onto alpha e_q (its dot products are
+// z - alpha J(:,q), so the add costs one sqrt) and appends [d(0:q); alpha] to R_A; dropping
+// constraint k re-triangularises R_A with Givens rotations applied to J's columns.
+// Registers: lane i holds row i of J, row i of R_A, 1/R_A(i,i), the multiplier and id of active
+// constraint i, and x_i; d is distributed (lane k holds d_k) through one LDS dump of J's rows in
+// the normal's support.  Starts from the unconstrained minimiser xm.  Wave-uniform control flow.
+template <int MAXM>
+__device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, const RowCons& rc,
+                     double xm, double tol, int maxit, int* st
 #ifdef MPCT_PROFILE
                      , unsigned long long* pacc, unsigned long long& pprev
 #endif
@@ -224,24 +266,37 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
   const bool row = lane < M;
   const double* sRi = lds + L.rinv;
   double* sxc = lds + L.xc;
-  double* sRA = lds + L.ra;  // R_A, row-major with stride M
   double* sJ = lds + L.jd;   // row dumps of J
   double* sd = lds + L.dv;   // d
-  double* su = lds + L.mu;
   const double* suprev = lds + L.uprev;
-  int* sW = reinterpret_cast<int*>(lds + L.wid);
-  unsigned act = 0;  // active bits of this row's 4 constraints
+  unsigned act = 0;          // active bits of this row's 4 constraints
   int q = 0, it = 0;
   bool jinit = false;
-  double Jr[MAXM];
-  double xm = row ? sxc[lane] : 0.0;
+  double Jr[MAXM];           // row `lane` of J
+  double* sRA = lds + L.ra;  // R_A, row-major, stride M (columns = active constraints in order)
+  double rdg = 0.0;          // 1 / R_A(lane, lane)
+  double uw = 0.0;           // multiplier of active constraint `lane`
+  int ww = -1;               // id of active constraint `lane`
   const double up_row = row ? suprev[rc.n] : 0.0;
+  const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
   for (;;) {
+    // ---- most violated inactive constraint
+    const double pre = block_prefix<MAXM>(xm, rc.l, Nu, row, sxc);
     double best = INFINITY;
     int bid = 0x7fffffff;
     if (row) {
       double s[4];
-      row_slacks(sxc, lane, rc, up_row, s);
+      if (rc.l == 0) {
+        s[0] = xm - lo_box;
+        s[1] = hi_box - xm;
+        s[2] = INFINITY;
+        s[3] = INFINITY;
+      } else {
+        s[0] = xm - rc.dmin;
+        s[1] = rc.dmax - xm;
+        s[2] = pre - (rc.umin - up_row);
+        s[3] = (rc.umax - up_row) - pre;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (!((act >> k) & 1u) && s[k] < best) {
@@ -256,7 +311,7 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
-    if (!jinit) {  // J = R^-1
+    if (!jinit) {  // J = R^-1, R_A empty
 #pragma unroll
       for (int k = 0; k < MAXM; ++k) Jr[k] = (row && k < M) ? sRi[lane * M + k] : 0.0;
       jinit = true;
@@ -270,7 +325,7 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
     bool infeas = false;
     for (;;) {
       ++it;
-      // d = J'n_p = sg * (sum of J's rows j0..mp)
+      // ---- d = J'n_p = sg * (sum of J's rows j0..mp): dump those rows, lane k sums column k
       if (lane >= j0 && lane <= mp) {
 #pragma unroll
         for (int k = 0; k < MAXM; ++k)
@@ -283,28 +338,37 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
         dk *= sgp;
         sd[lane] = dk;
       }
-      const double dn2 = qsum<MAXM>(dk * dk);
-      const double beta = qsum<MAXM>(lane >= q ? dk * dk : 0.0);
+      const double d2 = dk * dk;
+      const double dn2 = qsum<MAXM>(d2);
+      const double beta = qsum<MAXM>(lane >= q ? d2 : 0.0);
       lds_sync();
-      PSTAMP(PROF_QD);
+      // ---- z = J(:,q:) d(q:)
       double zm = 0.0;
       if (row) {
+        double z0 = 0.0, z1 = 0.0;
 #pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k >= q && k < M) zm += Jr[k] * sd[k];
+        for (int k = 0; k < MAXM; k += 2) {
+          if (k >= q && k < M) z0 += Jr[k] * sd[k];
+          if (k + 1 >= q && k + 1 < M) z1 += Jr[k + 1] * sd[k + 1];
+        }
+        zm = z0 + z1;
       }
-      // r = R_A^-1 d(0:q): column-oriented back substitution, lane w holds r_w
+      PSTAMP(PROF_QD);
+      // ---- r = R_A^-1 d(0:q): column back substitution, lane w ends with r_w
       double ck = lane < q ? dk : 0.0, rk = 0.0;
-      for (int w = q - 1; w >= 0; --w) {
-        const double rw = bcast(ck, w) / sRA[w * M + w];
-        if (lane == w) rk = rw;
-        if (lane < w) ck -= sRA[lane * M + w] * rw;
+#pragma unroll
+      for (int w = MAXM - 1; w >= 0; --w) {
+        if (w < q) {
+          const double rw = bcast(ck * rdg, w);
+          if (lane == w) rk = rw;
+          if (lane < w) ck -= sRA[lane * M + w] * rw;
+        }
       }
       // dual step over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
       if (lane < q && rk > 0.0) {
-        t1 = su[lane] / rk;
+        t1 = uw / rk;
         kdrop = lane;
       }
       qargmin<MAXM>(t1, kdrop);
@@ -317,39 +381,35 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
       }
       const bool full = t2 <= t1;
       const double t = full ? t2 : t1;
-      if (row && t2 != INFINITY) {
-        xm += t * zm;
-        sxc[lane] = xm;
-      }
-      if (lane < q) su[lane] -= t * rk;
+      if (t2 != INFINITY) xm += t * zm;
+      if (lane < q) uw -= t * rk;
       upm += t;
       sp += t * beta;
       if (full) {
-        // rotate d(q:) onto d(q), same rotations on J's columns (running value carried down)
-        double carry = sd[M - 1];
+        // ---- add p: Householder H = I - v v'/(v'v/2) on J(:,q:), v = d(q:) - alpha e_q
+        const double dq = bcast(dk, q);
+        const double nrm = sqrt(beta);
+        const double alpha = dq > 0.0 ? -nrm : nrm;
+        const double vq = dq - alpha;
+        const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
+        if (row) {
+          double jq = 0.0;
 #pragma unroll
-        for (int k = MAXM - 1; k >= 1; --k) {
-          if (k > q && k < M) {
-            const double a = sd[k - 1];
-            if (carry != 0.0) {
-              const double rho = sqrt(a * a + carry * carry);
-              const double ri = 1.0 / rho;
-              const double cs = a * ri, sn = carry * ri;
-              const double j0v = Jr[k - 1], j1v = Jr[k];
-              Jr[k - 1] = cs * j0v + sn * j1v;
-              Jr[k] = -sn * j0v + cs * j1v;
-              carry = rho;
-            } else {
-              carry = a;
-            }
+          for (int k = 0; k < MAXM; ++k)
+            if (k == q) jq = Jr[k];
+          const double f = (zm - alpha * jq) * two_vtv;
+#pragma unroll
+          for (int k = 0; k < MAXM; ++k) {
+            if (k >= q && k < M) Jr[k] -= f * (k == q ? vq : sd[k]);
           }
         }
-        // new column q of R_A = [d(0:q-1); carry]
+        // new column q of R_A = [d(0:q-1); alpha]
         if (lane < q) sRA[lane * M + q] = dk;
         if (lane == q) {
-          sRA[q * M + q] = carry;
-          su[q] = upm;
-          sW[q] = p;
+          sRA[q * M + q] = alpha;
+          rdg = 1.0 / alpha;
+          uw = upm;
+          ww = p;
         }
         if (lane == mp) act |= 1u << kindp;
         ++q;
@@ -359,28 +419,30 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
       }
       // ---- drop constraint kdrop: remove its column of R_A, re-triangularise with Givens
       const int kd = kdrop;
-      lds_sync();
-      const int idk = sW[kd];
+      const int idk = __builtin_amdgcn_readlane(ww, kd);
       if (lane == (idk >> 2)) act &= ~(1u << (idk & 3));
-      if (lane < q) {  // shift columns kd+1..q-1 left (lanes = rows)
+      if (lane < q) {  // remove column kd (lanes = rows)
         for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
       }
-      if (lane == 0) {
-        for (int w = kd; w < q - 1; ++w) {
-          su[w] = su[w + 1];
-          sW[w] = sW[w + 1];
+      {
+        const double un = lane_next<MAXM>(uw);
+        const int wn = lane_next_i<MAXM>(ww);
+        if (lane >= kd && lane < q - 1) {
+          uw = un;
+          ww = wn;
         }
       }
       lds_sync();
+      // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
 #pragma unroll
       for (int jj = 0; jj < MAXM - 1; ++jj) {
         if (jj >= kd && jj < q - 1) {
           const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
-          if (b != 0.0) {
-            const double rho = sqrt(a * a + b * b);
+          const double rho = sqrt(a * a + b * b);
+          if (rho != 0.0) {
             const double ri = 1.0 / rho;
             const double cs = a * ri, sn = b * ri;
-            if (lane >= jj && lane < q - 1) {  // rows jj, jj+1 of R_A (lanes = columns)
+            if (lane >= jj && lane < q - 1) {
               const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
               sRA[jj * M + lane] = cs * r0 + sn * r1;
               sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
@@ -393,6 +455,13 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
         }
       }
       --q;
+      if (lane < M) sRA[q * M + lane] = 0.0;  // the vacated row
+      if (lane == q) {
+        uw = 0.0;
+        ww = -1;
+      }
+      if (lane < q) rdg = 1.0 / sRA[lane * M + lane];
+      lds_sync();
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;
@@ -401,6 +470,7 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, const 
     }
     if (it >= maxit || infeas) break;
   }
+  if (row) sxc[lane] = xm;
   lds_sync();
   return it;
 }
@@ -612,6 +682,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
 
   // unconstrained minimiser dU = A x, then the QP; result in sxc
   auto solve_step = [&]() {
+    double xu = 0.0;
     if (lane < M) {
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       int s = 0;
@@ -622,12 +693,13 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
         a3 += sA[(s + 3) * M + lane] * sx[s + 3];
       }
       for (; s < nx; ++s) a0 += sA[s * M + lane] * sx[s];
-      sxc[lane] = (a0 + a1) + (a2 + a3);
+      xu = (a0 + a1) + (a2 + a3);
+      sxc[lane] = xu;
     }
     lds_sync();
     PSTAMP(PROF_UNC);
 #ifndef MPCT_EXP_NOQP
-    iters += gi_qp<MAXM>(lds, L, M, rcn, tol, maxit, &st
+    iters += gi_qp<MAXM>(lds, L, M, Nu, rcn, xu, tol, maxit, &st
 #ifdef MPCT_PROFILE
                          , pacc, pprev
 #endif
