@@ -29,7 +29,7 @@
 namespace mpct {
 
 struct LdsLayout {
-  int rinv, jd, dv, ra, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, wid, mu, step, total;
+  int rinv, jd, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, step, total;
 };
 
 __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, int ne, int my,
@@ -40,7 +40,8 @@ __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, 
   L.rinv = take(M * M);
   L.jd = take(M * M);        // row dumps of J (active-set method)
   L.dv = take(M);            // d = J'n_p
-  L.ra = take(M * M);        // R_A of the active-set method
+  L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
+  L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
   L.A = take(nx * M);
   L.x = take(nx);
   L.xc = take(M);
@@ -52,8 +53,6 @@ __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, 
   L.uring = take(2 * nin * kURing);
   L.plb = take(ne * plb);
   L.pla = take(ne * pla);
-  L.wid = take(M);
-  L.mu = take(M);
   L.step = take(my * nu * tlen > M * M ? my * nu * tlen : M * M);  // prologue only
   L.total = (o + 1) & ~1;
   return L;
@@ -252,12 +251,197 @@ __device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row
 // Householder reflector to J(:,q:) mapping d(q:) onto alpha e_q (its dot products are
 // z - alpha J(:,q), so the add costs one sqrt) and appends [d(0:q); alpha] to R_A; dropping
 // constraint k re-triangularises R_A with Givens rotations applied to J's columns.
-// Registers: lane i holds row i of J, row i of R_A, 1/R_A(i,i), the multiplier and id of active
-// constraint i, and x_i; d is distributed (lane k holds d_k) through one LDS dump of J's rows in
-// the normal's support.  Starts from the unconstrained minimiser xm.  Wave-uniform control flow.
+//
+// Warm start across the receding-horizon steps: the constraint normals do not depend on the
+// step (only the bounds do), so the factorisation of the previous step's final active set is
+// kept (J in registers, R_A in LDS).  Each QP first solves the equality-constrained problem on
+// that set from the unconstrained minimiser x_u (x = x_u + J_A w, R_A'w = b_A - N_A'x_u,
+// lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
+// and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
+// convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
+// R^-1 (re-adding the set) after 4M rotations, which bounds the orthogonality drift of the
+// rotated J (unbounded drift measured 3.5e-5 relative on the metric grid; with the rebuild
+// 7.5e-10).
 template <int MAXM>
-__device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, const RowCons& rc,
-                     double xm, double tol, int maxit, int* st
+struct GIState {
+  double Jr[MAXM];  // row `lane` of J
+  double rdg;       // 1 / R_A(lane, lane)
+  double uw;        // multiplier of active constraint `lane`
+  int ww;           // id (4*m + kind) of active constraint `lane`
+  unsigned act;     // active bits of this lane's 4 constraints (row m = lane)
+  int q;            // active-set size (wave-uniform)
+  int nrot;         // rotations applied to J since it was last built from R^-1 (uniform)
+  bool jinit;       // J holds a factorisation consistent with the active set (uniform)
+};
+
+template <int MAXM>
+__device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
+#pragma unroll
+  for (int k = 0; k < MAXM; ++k) S.Jr[k] = 0.0;
+  S.rdg = 0.0;
+  S.uw = 0.0;
+  S.ww = -1;
+  S.act = 0;
+  S.q = 0;
+  S.nrot = 0;
+  S.jinit = false;
+}
+
+template <int MAXM>
+__device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, const double* sRi, int M, bool row) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < MAXM; ++k) S.Jr[k] = (row && k < M) ? sRi[lane * M + k] : 0.0;
+  S.nrot = 0;
+  S.jinit = true;
+}
+
+// d = J'n_p = sg * (sum of J's rows j0..mp): dump those rows, lane k sums column k; d -> sd.
+template <int MAXM>
+__device__ __forceinline__ double gi_dvec(const GIState<MAXM>& S, double* sJ, double* sd, int M,
+                                          int j0, int mp, double sg, bool row) {
+  const int lane = threadIdx.x;
+  if (lane >= j0 && lane <= mp) {
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+      if (k < M) sJ[lane * M + k] = S.Jr[k];
+  }
+  lds_sync();
+  double dk = 0.0;
+  if (row) {
+    for (int j = j0; j <= mp; ++j) dk += sJ[j * M + lane];
+    dk *= sg;
+    sd[lane] = dk;
+  }
+  return dk;
+}
+
+// z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
+template <int MAXM>
+__device__ __forceinline__ double gi_z(const GIState<MAXM>& S, const double* sd, int q, int M, bool row) {
+  double z0 = 0.0, z1 = 0.0;
+  if (row) {
+#pragma unroll
+    for (int k = 0; k < MAXM; k += 2) {
+      if (k >= q && k < M) z0 += S.Jr[k] * sd[k];
+      if (k + 1 >= q && k + 1 < M) z1 += S.Jr[k + 1] * sd[k + 1];
+    }
+  }
+  return z0 + z1;
+}
+
+// r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
+template <int MAXM>
+__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
+  const int lane = threadIdx.x;
+  double ck = lane < S.q ? c : 0.0, rk = 0.0;
+#pragma unroll
+  for (int w = MAXM - 1; w >= 0; --w) {
+    if (w < S.q) {
+      const double rw = bcast(ck * S.rdg, w);
+      if (lane == w) rk = rw;
+      if (lane < w) ck -= sRA[lane * M + w] * rw;
+    }
+  }
+  return rk;
+}
+
+// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
+template <int MAXM>
+__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sRA, const double* sd, int M, int p,
+                                       double dk, double beta, double zm, double upm, bool row) {
+  const int lane = threadIdx.x;
+  const int q = S.q;
+  const double dq = bcast(dk, q);
+  const double nrm = sqrt(beta);
+  const double alpha = dq > 0.0 ? -nrm : nrm;
+  const double vq = dq - alpha;
+  const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
+  if (row) {
+    double jq = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+      if (k == q) jq = S.Jr[k];
+    const double f = (zm - alpha * jq) * two_vtv;
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+      if (k >= q && k < M) S.Jr[k] -= f * (k == q ? vq : sd[k]);
+  }
+  if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  if (lane == q) {
+    sRA[q * M + q] = alpha;
+    S.rdg = 1.0 / alpha;
+    S.uw = upm;
+    S.ww = p;
+  }
+  if (lane == (p >> 2)) S.act |= 1u << (p & 3);
+  S.q = q + 1;
+  S.nrot += 1;
+  lds_sync();
+}
+
+// remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
+template <int MAXM>
+__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sRA, int M, int kd) {
+  const int lane = threadIdx.x;
+  const int q = S.q;
+  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
+  if (lane == (idk >> 2)) S.act &= ~(1u << (idk & 3));
+  if (lane < q) {  // remove column kd (lanes = rows)
+    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
+  }
+  {
+    const double un = lane_next<MAXM>(S.uw);
+    const int wn = lane_next_i<MAXM>(S.ww);
+    if (lane >= kd && lane < q - 1) {
+      S.uw = un;
+      S.ww = wn;
+    }
+  }
+  lds_sync();
+  // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
+#pragma unroll
+  for (int jj = 0; jj < MAXM - 1; ++jj) {
+    if (jj >= kd && jj < q - 1) {
+      const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
+      const double rho = sqrt(a * a + b * b);
+      if (rho != 0.0) {
+        const double ri = 1.0 / rho;
+        const double cs = a * ri, sn = b * ri;
+        if (lane >= jj && lane < q - 1) {
+          const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
+          sRA[jj * M + lane] = cs * r0 + sn * r1;
+          sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
+        }
+        const double j0v = S.Jr[jj], j1v = S.Jr[jj + 1];
+        S.Jr[jj] = cs * j0v + sn * j1v;
+        S.Jr[jj + 1] = -sn * j0v + cs * j1v;
+        S.nrot += 1;
+      }
+      lds_sync();
+    }
+  }
+  const int qn = q - 1;
+  if (lane == qn) {
+    S.uw = 0.0;
+    S.ww = -1;
+  }
+  if (lane < qn) S.rdg = 1.0 / sRA[lane * M + lane];
+  S.q = qn;
+  lds_sync();
+}
+
+// normal of constraint p = 4m + kind: rows j0..m of the MV block, sign
+__device__ __forceinline__ void gi_normal(int p, const RowCons& rc, int& j0, int& mp, double& sg) {
+  mp = p >> 2;
+  const int kind = p & 3;
+  j0 = kind < 2 ? mp : mp - __builtin_amdgcn_readlane(rc.l, mp);
+  sg = (kind & 1) ? -1.0 : 1.0;
+}
+
+template <int MAXM>
+__device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, const RowCons& rc,
+                     double xu, double tol, int maxit, int* st, GIState<MAXM>& S
 #ifdef MPCT_PROFILE
                      , unsigned long long* pacc, unsigned long long& pprev
 #endif
@@ -266,40 +450,117 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
   const bool row = lane < M;
   const double* sRi = lds + L.rinv;
   double* sxc = lds + L.xc;
-  double* sJ = lds + L.jd;   // row dumps of J
-  double* sd = lds + L.dv;   // d
+  double* sJ = lds + L.jd;
+  double* sd = lds + L.dv;
+  double* sRA = lds + L.ra;
+  double* ssl = lds + L.sl;
   const double* suprev = lds + L.uprev;
-  unsigned act = 0;          // active bits of this row's 4 constraints
-  int q = 0, it = 0;
-  bool jinit = false;
-  double Jr[MAXM];           // row `lane` of J
-  double* sRA = lds + L.ra;  // R_A, row-major, stride M (columns = active constraints in order)
-  double rdg = 0.0;          // 1 / R_A(lane, lane)
-  double uw = 0.0;           // multiplier of active constraint `lane`
-  int ww = -1;               // id of active constraint `lane`
   const double up_row = row ? suprev[rc.n] : 0.0;
   const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
+  auto slacks = [&](double x, double s[4]) {
+    const double pre = block_prefix<MAXM>(x, rc.l, Nu, row, sxc);
+    if (rc.l == 0) {
+      s[0] = x - lo_box;
+      s[1] = hi_box - x;
+      s[2] = INFINITY;
+      s[3] = INFINITY;
+    } else {
+      s[0] = x - rc.dmin;
+      s[1] = rc.dmax - x;
+      s[2] = pre - (rc.umin - up_row);
+      s[3] = (rc.umax - up_row) - pre;
+    }
+    if (!row) s[0] = s[1] = s[2] = s[3] = INFINITY;
+  };
+  int it = 0;
+  double xm = xu;
+  {
+    // the unconstrained minimiser is optimal when it is feasible (the retained set is kept)
+    double s[4];
+    slacks(xu, s);
+    double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
+    int dummy = lane;
+    qargmin<MAXM>(smin, dummy);
+    if (!(smin < -tol)) {
+      if (row) sxc[lane] = xu;
+      lds_sync();
+      return 0;
+    }
+    if (S.q == 0) {
+      S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
+    } else {
+      if (row) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
+      }
+      if (!S.jinit || S.nrot >= 4 * M) {
+        // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
+        const int qq = S.q;
+        gi_load_rinv<MAXM>(S, sRi, M, row);
+        S.q = 0;
+        for (int v = 0; v < qq; ++v) {
+          const int p = __builtin_amdgcn_readlane(S.ww, v);
+          int j0, mp;
+          double sg;
+          gi_normal(p, rc, j0, mp, sg);
+          const double dk = gi_dvec<MAXM>(S, sJ, sd, M, j0, mp, sg, row);
+          const double beta = qsum<MAXM>(lane >= v ? dk * dk : 0.0);
+          lds_sync();
+          const double zm = gi_z<MAXM>(S, sd, v, M, row);
+          const double uk = S.uw;
+          gi_add<MAXM>(S, sRA, sd, M, p, dk, beta, zm, 0.0, row);
+          if (lane == v) S.uw = uk;
+          ++it;
+        }
+        S.nrot = 0;
+      }
+      lds_sync();
+      // equality-constrained solve on the retained set, dropping negative multipliers
+      for (;;) {
+        const int q = S.q;
+        if (q == 0) {
+          xm = xu;
+          break;
+        }
+        double c = 0.0;
+        if (lane < q) c = -ssl[S.ww];  // b_A - N_A'x_u
+        double wv = 0.0;
+        xm = xu;
+#pragma unroll
+        for (int v = 0; v < MAXM; ++v) {
+          if (v < q) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
+            const double w = bcast(c * S.rdg, v);
+            if (lane == v) wv = w;
+            if (lane > v && lane < q) c -= sRA[v * M + lane] * w;
+            xm += S.Jr[v] * w;
+          }
+        }
+        const double lam = gi_backsub<MAXM>(S, sRA, M, wv);
+        if (lane < q) S.uw = lam;
+        double lmin = lane < q ? lam : INFINITY;
+        int kd = lane;
+        qargmin<MAXM>(lmin, kd);
+        if (!(lmin < 0.0)) break;
+        gi_drop<MAXM>(S, sRA, M, kd);
+        ++it;
+      }
+      if (!row) xm = 0.0;
+    }
+  }
+  PSTAMP(PROF_QWARM);
+#ifdef MPCT_DEBUG_SIM
+  if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0) printf("QP entry-after-warm q=%d it=%d nrot=%d\n", S.q, it, S.nrot);
+#endif
   for (;;) {
     // ---- most violated inactive constraint
-    const double pre = block_prefix<MAXM>(xm, rc.l, Nu, row, sxc);
     double best = INFINITY;
     int bid = 0x7fffffff;
-    if (row) {
+    {
       double s[4];
-      if (rc.l == 0) {
-        s[0] = xm - lo_box;
-        s[1] = hi_box - xm;
-        s[2] = INFINITY;
-        s[3] = INFINITY;
-      } else {
-        s[0] = xm - rc.dmin;
-        s[1] = rc.dmax - xm;
-        s[2] = pre - (rc.umin - up_row);
-        s[3] = (rc.umax - up_row) - pre;
-      }
+      slacks(xm, s);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (!((act >> k) & 1u) && s[k] < best) {
+        if (!((S.act >> k) & 1u) && s[k] < best) {
           best = s[k];
           bid = 4 * lane + k;
         }
@@ -307,68 +568,33 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
     qargmin<MAXM>(best, bid);
     PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
-    if (it >= maxit || q >= M) {
+    if (it >= maxit || S.q >= M) {
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
-    if (!jinit) {  // J = R^-1, R_A empty
-#pragma unroll
-      for (int k = 0; k < MAXM; ++k) Jr[k] = (row && k < M) ? sRi[lane * M + k] : 0.0;
-      jinit = true;
-    }
+    if (!S.jinit) gi_load_rinv<MAXM>(S, sRi, M, row);
     const int p = bid;
-    const int mp = p >> 2, kindp = p & 3;
-    const int j0 = kindp < 2 ? mp : mp - __builtin_amdgcn_readlane(rc.l, mp);
-    const double sgp = (kindp & 1) ? -1.0 : 1.0;
+    int j0, mp;
+    double sgp;
+    gi_normal(p, rc, j0, mp, sgp);
     double sp = best;  // slack of p along the path
     double upm = 0.0;  // its multiplier
     bool infeas = false;
     for (;;) {
       ++it;
-      // ---- d = J'n_p = sg * (sum of J's rows j0..mp): dump those rows, lane k sums column k
-      if (lane >= j0 && lane <= mp) {
-#pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k < M) sJ[lane * M + k] = Jr[k];
-      }
-      lds_sync();
-      double dk = 0.0;
-      if (row) {
-        for (int j = j0; j <= mp; ++j) dk += sJ[j * M + lane];
-        dk *= sgp;
-        sd[lane] = dk;
-      }
+      const double dk = gi_dvec<MAXM>(S, sJ, sd, M, j0, mp, sgp, row);
       const double d2 = dk * dk;
       const double dn2 = qsum<MAXM>(d2);
-      const double beta = qsum<MAXM>(lane >= q ? d2 : 0.0);
+      const double beta = qsum<MAXM>(lane >= S.q ? d2 : 0.0);
       lds_sync();
-      // ---- z = J(:,q:) d(q:)
-      double zm = 0.0;
-      if (row) {
-        double z0 = 0.0, z1 = 0.0;
-#pragma unroll
-        for (int k = 0; k < MAXM; k += 2) {
-          if (k >= q && k < M) z0 += Jr[k] * sd[k];
-          if (k + 1 >= q && k + 1 < M) z1 += Jr[k + 1] * sd[k + 1];
-        }
-        zm = z0 + z1;
-      }
+      const double zm = gi_z<MAXM>(S, sd, S.q, M, row);
       PSTAMP(PROF_QD);
-      // ---- r = R_A^-1 d(0:q): column back substitution, lane w ends with r_w
-      double ck = lane < q ? dk : 0.0, rk = 0.0;
-#pragma unroll
-      for (int w = MAXM - 1; w >= 0; --w) {
-        if (w < q) {
-          const double rw = bcast(ck * rdg, w);
-          if (lane == w) rk = rw;
-          if (lane < w) ck -= sRA[lane * M + w] * rw;
-        }
-      }
+      const double rk = gi_backsub<MAXM>(S, sRA, M, dk);
       // dual step over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
-      if (lane < q && rk > 0.0) {
-        t1 = uw / rk;
+      if (lane < S.q && rk > 0.0) {
+        t1 = S.uw / rk;
         kdrop = lane;
       }
       qargmin<MAXM>(t1, kdrop);
@@ -381,87 +607,20 @@ __device__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu
       }
       const bool full = t2 <= t1;
       const double t = full ? t2 : t1;
+#ifdef MPCT_DEBUG_SIM
+      if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0 && it > 40 && it < 70)
+        printf("it=%d q=%d p=%d sp=%.3e beta=%.3e dn2=%.3e t1=%.3e t2=%.3e kd=%d %s\n", it, S.q, p, sp, beta, dn2, t1, t2, kdrop, full ? "ADD" : "DROP");
+#endif
       if (t2 != INFINITY) xm += t * zm;
-      if (lane < q) uw -= t * rk;
+      if (lane < S.q) S.uw -= t * rk;
       upm += t;
       sp += t * beta;
       if (full) {
-        // ---- add p: Householder H = I - v v'/(v'v/2) on J(:,q:), v = d(q:) - alpha e_q
-        const double dq = bcast(dk, q);
-        const double nrm = sqrt(beta);
-        const double alpha = dq > 0.0 ? -nrm : nrm;
-        const double vq = dq - alpha;
-        const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
-        if (row) {
-          double jq = 0.0;
-#pragma unroll
-          for (int k = 0; k < MAXM; ++k)
-            if (k == q) jq = Jr[k];
-          const double f = (zm - alpha * jq) * two_vtv;
-#pragma unroll
-          for (int k = 0; k < MAXM; ++k) {
-            if (k >= q && k < M) Jr[k] -= f * (k == q ? vq : sd[k]);
-          }
-        }
-        // new column q of R_A = [d(0:q-1); alpha]
-        if (lane < q) sRA[lane * M + q] = dk;
-        if (lane == q) {
-          sRA[q * M + q] = alpha;
-          rdg = 1.0 / alpha;
-          uw = upm;
-          ww = p;
-        }
-        if (lane == mp) act |= 1u << kindp;
-        ++q;
-        lds_sync();
+        gi_add<MAXM>(S, sRA, sd, M, p, dk, beta, zm, upm, row);
         PSTAMP(PROF_QADD);
         break;
       }
-      // ---- drop constraint kdrop: remove its column of R_A, re-triangularise with Givens
-      const int kd = kdrop;
-      const int idk = __builtin_amdgcn_readlane(ww, kd);
-      if (lane == (idk >> 2)) act &= ~(1u << (idk & 3));
-      if (lane < q) {  // remove column kd (lanes = rows)
-        for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
-      }
-      {
-        const double un = lane_next<MAXM>(uw);
-        const int wn = lane_next_i<MAXM>(ww);
-        if (lane >= kd && lane < q - 1) {
-          uw = un;
-          ww = wn;
-        }
-      }
-      lds_sync();
-      // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
-#pragma unroll
-      for (int jj = 0; jj < MAXM - 1; ++jj) {
-        if (jj >= kd && jj < q - 1) {
-          const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
-          const double rho = sqrt(a * a + b * b);
-          if (rho != 0.0) {
-            const double ri = 1.0 / rho;
-            const double cs = a * ri, sn = b * ri;
-            if (lane >= jj && lane < q - 1) {
-              const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
-              sRA[jj * M + lane] = cs * r0 + sn * r1;
-              sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
-            }
-            const double j0v = Jr[jj], j1v = Jr[jj + 1];
-            Jr[jj] = cs * j0v + sn * j1v;
-            Jr[jj + 1] = -sn * j0v + cs * j1v;
-          }
-          lds_sync();
-        }
-      }
-      --q;
-      if (lane < M) sRA[q * M + lane] = 0.0;  // the vacated row
-      if (lane == q) {
-        uw = 0.0;
-        ww = -1;
-      }
-      if (lane < q) rdg = 1.0 / sRA[lane * M + lane];
-      lds_sync();
+      gi_drop<MAXM>(S, sRA, M, kdrop);
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;
@@ -498,7 +657,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 
-  auto write_nan = [&](int status) {
+  auto write_nan = [&](int status) __attribute__((always_inline)) {
     if (lane < my) {
       if (out.J1) out.J1[sim * my + lane] = NAN;
       if (out.j21) out.j21[sim * my + lane] = NAN;
@@ -680,8 +839,10 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   const double* rr = rv + (long long)kref * my * nit;
   const double* vvk = vv ? vv + (long long)kref * sc.nd * nit : nullptr;
 
+  GIState<MAXM> gis;  // active-set factorisation carried across the steps (warm start)
+  gi_reset<MAXM>(gis);
   // unconstrained minimiser dU = A x, then the QP; result in sxc
-  auto solve_step = [&]() {
+  auto solve_step = [&]() __attribute__((always_inline)) {
     double xu = 0.0;
     if (lane < M) {
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
@@ -699,7 +860,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     lds_sync();
     PSTAMP(PROF_UNC);
 #ifndef MPCT_EXP_NOQP
-    iters += gi_qp<MAXM>(lds, L, M, Nu, rcn, xu, tol, maxit, &st
+    iters += gi_qp<MAXM>(lds, L, M, Nu, rcn, xu, tol, maxit, &st, gis
 #ifdef MPCT_PROFILE
                          , pacc, pprev
 #endif

@@ -496,7 +496,7 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
         mx[k] = std::max(mx[k], (double)hp[i * PROF_N + k]);
       }
     const char* nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
-                              "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop"};
+                              "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm"};
     fprintf(stderr, "[mpct profile] mean / max cycles per simulation over %lld sims\n", S);
     for (int k = 0; k < PROF_N; ++k)
       fprintf(stderr, "  %-14s %12.0f %12.0f\n", nm[k], sum[k] / (double)S, mx[k]);
