@@ -149,3 +149,28 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(OSError):
         _lib.load()
+
+
+def _kernel_meta(text):
+    out = {}
+    for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, flags=re.S):
+        body = m.group(2)
+        maxm = int(re.search(r"kernelILi(\d+)E", m.group(1)).group(1))
+        out[maxm] = dict(
+            scratch=int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", body).group(1)),
+            vgpr=int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", body).group(1)))
+    return out
+
+
+def test_kernel_isa_invariants(built):
+    """The single-wave LDS hand-offs (lds_sync = lgkmcnt(0)) require every helper inlined and no
+    LDS access lowered to FLAT (a non-inlined gi_qp once raced this way at -O3).  The metric
+    size class (M <= 16) must also run without scratch and at 2 waves/SIMD (<= 256 VGPRs)."""
+    import __graft_entry__ as g
+
+    text = open(g.kernel_isa()).read()
+    assert "s_swappc_b64" not in text
+    assert "flat_load" not in text and "flat_store" not in text
+    meta = _kernel_meta(text)
+    assert set(meta) == {16, 32, 64}
+    assert meta[16]["scratch"] == 0 and meta[16]["vgpr"] <= 256, meta[16]
