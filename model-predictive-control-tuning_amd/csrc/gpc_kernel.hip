@@ -29,7 +29,7 @@
 namespace mpct {
 
 struct LdsLayout {
-  int rinv, jd, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, step, total;
+  int rinv, jt, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, step, total;
 };
 
 __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, int ne, int my,
@@ -38,7 +38,7 @@ __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, 
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.rinv = take(M * M);
-  L.jd = take(M * M);        // row dumps of J (active-set method)
+  L.jt = take(M * M);        // J of the active-set method, column-major JT[k*M + i] = J(i,k)
   L.dv = take(M);            // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
@@ -264,7 +264,6 @@ __device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row
 // 7.5e-10).
 template <int MAXM>
 struct GIState {
-  double Jr[MAXM];  // row `lane` of J
   double rdg;       // 1 / R_A(lane, lane)
   double uw;        // multiplier of active constraint `lane`
   int ww;           // id (4*m + kind) of active constraint `lane`
@@ -276,8 +275,6 @@ struct GIState {
 
 template <int MAXM>
 __device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
-#pragma unroll
-  for (int k = 0; k < MAXM; ++k) S.Jr[k] = 0.0;
   S.rdg = 0.0;
   S.uw = 0.0;
   S.ww = -1;
@@ -288,28 +285,24 @@ __device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
 }
 
 template <int MAXM>
-__device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, const double* sRi, int M, bool row) {
+__device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
+                                             bool row) {
   const int lane = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < MAXM; ++k) S.Jr[k] = (row && k < M) ? sRi[lane * M + k] : 0.0;
+  if (row)
+    for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
   S.nrot = 0;
   S.jinit = true;
+  lds_sync();
 }
 
-// d = J'n_p = sg * (sum of J's rows j0..mp): dump those rows, lane k sums column k; d -> sd.
+// d = J'n_p = sg * (sum of J's rows j0..mp): lane k sums column k of J (contiguous in JT); d -> sd
 template <int MAXM>
-__device__ __forceinline__ double gi_dvec(const GIState<MAXM>& S, double* sJ, double* sd, int M,
-                                          int j0, int mp, double sg, bool row) {
+__device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, int j0, int mp, double sg,
+                                          bool row) {
   const int lane = threadIdx.x;
-  if (lane >= j0 && lane <= mp) {
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k)
-      if (k < M) sJ[lane * M + k] = S.Jr[k];
-  }
-  lds_sync();
   double dk = 0.0;
   if (row) {
-    for (int j = j0; j <= mp; ++j) dk += sJ[j * M + lane];
+    for (int j = j0; j <= mp; ++j) dk += sJT[lane * M + j];
     dk *= sg;
     sd[lane] = dk;
   }
@@ -317,15 +310,16 @@ __device__ __forceinline__ double gi_dvec(const GIState<MAXM>& S, double* sJ, do
 }
 
 // z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
-template <int MAXM>
-__device__ __forceinline__ double gi_z(const GIState<MAXM>& S, const double* sd, int q, int M, bool row) {
+__device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row) {
+  const int lane = threadIdx.x;
   double z0 = 0.0, z1 = 0.0;
   if (row) {
-#pragma unroll
-    for (int k = 0; k < MAXM; k += 2) {
-      if (k >= q && k < M) z0 += S.Jr[k] * sd[k];
-      if (k + 1 >= q && k + 1 < M) z1 += S.Jr[k + 1] * sd[k + 1];
+    int k = q;
+    for (; k + 1 < M; k += 2) {
+      z0 += sJT[k * M + lane] * sd[k];
+      z1 += sJT[(k + 1) * M + lane] * sd[k + 1];
     }
+    if (k < M) z0 += sJT[k * M + lane] * sd[k];
   }
   return z0 + z1;
 }
@@ -335,21 +329,18 @@ template <int MAXM>
 __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
   const int lane = threadIdx.x;
   double ck = lane < S.q ? c : 0.0, rk = 0.0;
-#pragma unroll
-  for (int w = MAXM - 1; w >= 0; --w) {
-    if (w < S.q) {
-      const double rw = bcast(ck * S.rdg, w);
-      if (lane == w) rk = rw;
-      if (lane < w) ck -= sRA[lane * M + w] * rw;
-    }
+  for (int w = S.q - 1; w >= 0; --w) {
+    const double rw = bcast(ck * S.rdg, w);
+    if (lane == w) rk = rw;
+    if (lane < w) ck -= sRA[lane * M + w] * rw;
   }
   return rk;
 }
 
 // append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
 template <int MAXM>
-__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sRA, const double* sd, int M, int p,
-                                       double dk, double beta, double zm, double upm, bool row) {
+__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
+                                       int p, double dk, double beta, double zm, double upm, bool row) {
   const int lane = threadIdx.x;
   const int q = S.q;
   const double dq = bcast(dk, q);
@@ -358,14 +349,10 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sRA, const doub
   const double vq = dq - alpha;
   const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
   if (row) {
-    double jq = 0.0;
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k)
-      if (k == q) jq = S.Jr[k];
+    const double jq = sJT[q * M + lane];
     const double f = (zm - alpha * jq) * two_vtv;
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k)
-      if (k >= q && k < M) S.Jr[k] -= f * (k == q ? vq : sd[k]);
+    sJT[q * M + lane] = jq - f * vq;
+    for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
   if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
   if (lane == q) {
@@ -382,7 +369,7 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sRA, const doub
 
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
 template <int MAXM>
-__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sRA, int M, int kd) {
+__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd) {
   const int lane = threadIdx.x;
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
@@ -400,9 +387,8 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sRA, int M, in
   }
   lds_sync();
   // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
-#pragma unroll
-  for (int jj = 0; jj < MAXM - 1; ++jj) {
-    if (jj >= kd && jj < q - 1) {
+  for (int jj = kd; jj < q - 1; ++jj) {
+    {
       const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
       const double rho = sqrt(a * a + b * b);
       if (rho != 0.0) {
@@ -413,9 +399,11 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sRA, int M, in
           sRA[jj * M + lane] = cs * r0 + sn * r1;
           sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
         }
-        const double j0v = S.Jr[jj], j1v = S.Jr[jj + 1];
-        S.Jr[jj] = cs * j0v + sn * j1v;
-        S.Jr[jj + 1] = -sn * j0v + cs * j1v;
+        if (lane < M) {
+          const double j0v = sJT[jj * M + lane], j1v = sJT[(jj + 1) * M + lane];
+          sJT[jj * M + lane] = cs * j0v + sn * j1v;
+          sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
+        }
         S.nrot += 1;
       }
       lds_sync();
@@ -450,7 +438,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
   const bool row = lane < M;
   const double* sRi = lds + L.rinv;
   double* sxc = lds + L.xc;
-  double* sJ = lds + L.jd;
+  double* sJT = lds + L.jt;
   double* sd = lds + L.dv;
   double* sRA = lds + L.ra;
   double* ssl = lds + L.sl;
@@ -496,19 +484,19 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
       if (!S.jinit || S.nrot >= 4 * M) {
         // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
-        gi_load_rinv<MAXM>(S, sRi, M, row);
+        gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
         S.q = 0;
         for (int v = 0; v < qq; ++v) {
           const int p = __builtin_amdgcn_readlane(S.ww, v);
           int j0, mp;
           double sg;
           gi_normal(p, rc, j0, mp, sg);
-          const double dk = gi_dvec<MAXM>(S, sJ, sd, M, j0, mp, sg, row);
+          const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sg, row);
           const double beta = qsum<MAXM>(lane >= v ? dk * dk : 0.0);
           lds_sync();
-          const double zm = gi_z<MAXM>(S, sd, v, M, row);
+          const double zm = gi_z(sJT, sd, v, M, row);
           const double uk = S.uw;
-          gi_add<MAXM>(S, sRA, sd, M, p, dk, beta, zm, 0.0, row);
+          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row);
           if (lane == v) S.uw = uk;
           ++it;
         }
@@ -526,14 +514,11 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
         if (lane < q) c = -ssl[S.ww];  // b_A - N_A'x_u
         double wv = 0.0;
         xm = xu;
-#pragma unroll
-        for (int v = 0; v < MAXM; ++v) {
-          if (v < q) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
-            const double w = bcast(c * S.rdg, v);
-            if (lane == v) wv = w;
-            if (lane > v && lane < q) c -= sRA[v * M + lane] * w;
-            xm += S.Jr[v] * w;
-          }
+        for (int v = 0; v < q; ++v) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
+          const double w = bcast(c * S.rdg, v);
+          if (lane == v) wv = w;
+          if (lane > v && lane < q) c -= sRA[v * M + lane] * w;
+          if (row) xm += sJT[v * M + lane] * w;
         }
         const double lam = gi_backsub<MAXM>(S, sRA, M, wv);
         if (lane < q) S.uw = lam;
@@ -541,7 +526,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(S, sRA, M, kd);
+        gi_drop<MAXM>(S, sJT, sRA, M, kd);
         ++it;
       }
       if (!row) xm = 0.0;
@@ -572,7 +557,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
-    if (!S.jinit) gi_load_rinv<MAXM>(S, sRi, M, row);
+    if (!S.jinit) gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
     const int p = bid;
     int j0, mp;
     double sgp;
@@ -582,12 +567,12 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
     bool infeas = false;
     for (;;) {
       ++it;
-      const double dk = gi_dvec<MAXM>(S, sJ, sd, M, j0, mp, sgp, row);
+      const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sgp, row);
       const double d2 = dk * dk;
       const double dn2 = qsum<MAXM>(d2);
       const double beta = qsum<MAXM>(lane >= S.q ? d2 : 0.0);
       lds_sync();
-      const double zm = gi_z<MAXM>(S, sd, S.q, M, row);
+      const double zm = gi_z(sJT, sd, S.q, M, row);
       PSTAMP(PROF_QD);
       const double rk = gi_backsub<MAXM>(S, sRA, M, dk);
       // dual step over active constraints with r_w > 0
@@ -616,11 +601,11 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
       upm += t;
       sp += t * beta;
       if (full) {
-        gi_add<MAXM>(S, sRA, sd, M, p, dk, beta, zm, upm, row);
+        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row);
         PSTAMP(PROF_QADD);
         break;
       }
-      gi_drop<MAXM>(S, sRA, M, kdrop);
+      gi_drop<MAXM>(S, sJT, sRA, M, kdrop);
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;
@@ -952,18 +937,13 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
-      double hist[kYeHist];
-#pragma unroll
-      for (int k = 1; k < kYeHist; ++k) hist[k] = k < nyh_i ? sx[yoff_i + k] : 0.0;
       double cur = y, prev = syprev[i];
-#pragma unroll
-      for (int k = 1; k < kYeHist; ++k) {
-        if (k < nyh_i) {
-          const double nk = cur - prev;
-          sx[yoff_i + k] = nk;
-          cur = nk;
-          prev = hist[k];
-        }
+      for (int k = 1; k < nyh_i; ++k) {
+        const double old = sx[yoff_i + k];
+        const double nk = cur - prev;
+        sx[yoff_i + k] = nk;
+        cur = nk;
+        prev = old;
       }
       syprev[i] = y;
       sx[yoff_i] = y - r_t;
@@ -987,12 +967,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
-      double h[kMaxDum];
-#pragma unroll
-      for (int k = 0; k < kMaxDum - 1; ++k) h[k] = k < dum_n - 1 ? sx[upoff_n + k] : 0.0;
-#pragma unroll
-      for (int k = 1; k < kMaxDum; ++k)
-        if (k < dum_n) sx[upoff_n + k] = h[k - 1];
+      for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
       sx[upoff_n] = du;
       sur[n * kURing + (t & (kURing - 1))] = un;
       if (o.want_traj) {
