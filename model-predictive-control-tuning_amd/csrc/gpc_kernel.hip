@@ -42,8 +42,8 @@ __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, 
   L.dv = take(M);            // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
-  L.A = take(nx * M);
-  L.x = take(nx);
+  L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
+  L.x = take(nx + 1);
   L.xc = take(M);
   L.uprev = take(nu);
   L.yprev = take(my);
@@ -466,10 +466,8 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
     // the unconstrained minimiser is optimal when it is feasible (the retained set is kept)
     double s[4];
     slacks(xu, s);
-    double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
-    int dummy = lane;
-    qargmin<MAXM>(smin, dummy);
-    if (!(smin < -tol)) {
+    const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
+    if (__ballot(smin < -tol) == 0) {
       if (row) sxc[lane] = xu;
       lds_sync();
       return 0;
@@ -663,6 +661,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     return;
   }
   const LdsLayout L = lds_layout(M, nx, nu, nin, ne, my, sc.tlen, sc.pl_maxb, sc.pl_maxa);
+  const int nxp = (nx + 1) & ~1;  // padded row length of A (x[nx] and the pad column are 0)
   double* sRi = lds + L.rinv;
   double* sA = lds + L.A;
   double* sx = lds + L.x;
@@ -699,6 +698,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   const int ej = ee % nin;
   const int e_nb = (lane < ne * 2) ? sc.pl_nb[ee] : 0;
   const int e_na = (lane < ne * 2) ? sc.pl_na[ee] : 0;
+  const int e_off = (lane < ne * 2) ? sc.pl_off[ee] : 0;
   const double* dl = deltav + c * my;
   const double* lm = lambdav + c * nu;
   lds_sync();
@@ -790,26 +790,17 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     }
 #pragma unroll
     for (int m = 0; m < MAXM; ++m)
-      if (m < M) sA[(lane - M) * M + m] = -rcol[m];
+      if (m < M) sA[m * nxp + (lane - M)] = -rcol[m];
   }
-  // R^-1 (upper): lane j solves R x = e_j; stored row-major, row m also kept in registers
+  if (lane < M && nxp > nx) sA[lane * nxp + nx] = 0.0;  // pad column
+  // R^-1 (upper, row-major): lane j solves R x = e_j in its own LDS column (zeros below)
   if (lane < M) {
-    double xr[MAXM];
-#pragma unroll
-    for (int kk = 0; kk < MAXM; ++kk) xr[kk] = 0.0;
-#pragma unroll
-    for (int kk = MAXM - 1; kk >= 0; --kk) {
-      if (kk < M && kk <= lane) {
-        double a = (kk == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int j = 0; j < MAXM; ++j)
-          if (j > kk && j < M) a -= sR[kk * M + j] * xr[j];
-        xr[kk] = a / sR[kk * M + kk];
-      }
+    for (int kk = lane; kk >= 0; --kk) {
+      double a = (kk == lane) ? 1.0 : 0.0;
+      for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[j * M + lane];
+      sRi[kk * M + lane] = a / sR[kk * M + kk];
     }
-#pragma unroll
-    for (int kk = 0; kk < MAXM; ++kk)
-      if (kk < M) sRi[kk * M + lane] = xr[kk];
+    for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
   }
   lds_sync();
   PSTAMP(PROF_PROLOGUE);
@@ -830,15 +821,24 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   auto solve_step = [&]() __attribute__((always_inline)) {
     double xu = 0.0;
     if (lane < M) {
+      // 16-byte LDS reads: two A entries of this row and two x entries per load
+      const double2* arow = reinterpret_cast<const double2*>(sA + lane * nxp);
+      const double2* xv = reinterpret_cast<const double2*>(sx);
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      int s = 0;
-      for (; s + 3 < nx; s += 4) {
-        a0 += sA[s * M + lane] * sx[s];
-        a1 += sA[(s + 1) * M + lane] * sx[s + 1];
-        a2 += sA[(s + 2) * M + lane] * sx[s + 2];
-        a3 += sA[(s + 3) * M + lane] * sx[s + 3];
+      int s2 = 0;
+      for (; s2 + 1 < nxp / 2; s2 += 2) {
+        const double2 av = arow[s2], bv = arow[s2 + 1];
+        const double2 xa = xv[s2], xb = xv[s2 + 1];
+        a0 += av.x * xa.x;
+        a1 += av.y * xa.y;
+        a2 += bv.x * xb.x;
+        a3 += bv.y * xb.y;
       }
-      for (; s < nx; ++s) a0 += sA[s * M + lane] * sx[s];
+      if (s2 < nxp / 2) {
+        const double2 av = arow[s2], xa = xv[s2];
+        a0 += av.x * xa.x;
+        a1 += av.y * xa.y;
+      }
       xu = (a0 + a1) + (a2 + a3);
       sxc[lane] = xu;
     }
@@ -917,15 +917,10 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
     if (is_entry) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
+      // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-      for (int l = 0; l < kMaxTaps; l += 2) {
-        if (l < e_nb) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
-        if (l + 1 < e_nb) a1 += eb[l + 1] * eur[(t - l - 1) & (kURing - 1)];
-      }
-#pragma unroll
-      for (int l = 1; l < kYeHist; ++l)
-        if (l < e_na) a0 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
+      for (int l = e_off; l < e_nb; ++l) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
+      for (int l = 1; l < e_na; ++l) a1 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
       const double acc = a0 + a1;
       eyh[t & (kYeHist - 1)] = acc;
       sye[lane] = acc;

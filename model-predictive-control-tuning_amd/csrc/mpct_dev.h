@@ -39,6 +39,7 @@ struct DevScenario {
   const int* dum;       // [nu]   duM_n
   const int* pl_nb;     // [ne]   plant entry numerator length (z^-1, delay folded in)
   const int* pl_na;     // [ne]   plant entry denominator length
+  const int* pl_off;    // [ne]   first nonzero numerator tap (the delay's leading zeros skipped)
   const double* pl_b;   // [ne][pl_maxb]
   const double* pl_a;   // [ne][pl_maxa]
   const double* bnd;    // [4][nu]  du_min, du_max, u_min, u_max

@@ -48,7 +48,7 @@ struct mpct_scenario {
   std::vector<double> phi;   // [my*n2max][nx]  reference layout (S | Hp)
   std::vector<double> phid;  // same rows on the device state basis (see create)
   int ne = 0, pl_maxb = 0, pl_maxa = 0;
-  std::vector<int> pl_nb, pl_na;
+  std::vector<int> pl_nb, pl_na, pl_off;
   std::vector<double> pl_b, pl_a;
   std::vector<double> bnd;   // [4][nu]
   std::vector<double> yref;  // [my][nit]
@@ -306,6 +306,12 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       s->pl_a[(size_t)e * s->pl_maxa + k] = p.den[k] / p.den[0];
     }
   }
+  s->pl_off.assign(s->ne, 0);
+  for (int e = 0; e < s->ne; ++e) {
+    int o = 0;
+    while (o < s->pl_nb[e] && s->pl_b[(size_t)e * s->pl_maxb + o] == 0.0) ++o;
+    s->pl_off[e] = o;
+  }
   s->bnd.resize(4 * nu);
   for (int n = 0; n < nu; ++n) {
     s->bnd[n] = d->du_min[n];
@@ -394,6 +400,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   size_t o_dum = put(s->dum.data(), s->dum.size() * 4);
   size_t o_plnb = put(s->pl_nb.data(), s->pl_nb.size() * 4);
   size_t o_plna = put(s->pl_na.data(), s->pl_na.size() * 4);
+  size_t o_ploff = put(s->pl_off.data(), s->pl_off.size() * 4);
   size_t o_plb = put(s->pl_b.data(), s->pl_b.size() * 8);
   size_t o_pla = put(s->pl_a.data(), s->pl_a.size() * 8);
   size_t o_bnd = put(s->bnd.data(), s->bnd.size() * 8);
@@ -431,6 +438,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.dum = reinterpret_cast<const int*>(b + o_dum);
   ds.pl_nb = reinterpret_cast<const int*>(b + o_plnb);
   ds.pl_na = reinterpret_cast<const int*>(b + o_plna);
+  ds.pl_off = reinterpret_cast<const int*>(b + o_ploff);
   ds.pl_b = reinterpret_cast<const double*>(b + o_plb);
   ds.pl_a = reinterpret_cast<const double*>(b + o_pla);
   ds.bnd = reinterpret_cast<const double*>(b + o_bnd);
