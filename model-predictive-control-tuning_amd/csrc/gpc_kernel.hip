@@ -721,44 +721,56 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     gn = lane / Nu;
     gc = lane - gn * Nu;
   }
-  for (int i = 0; i < my; ++i) {
+  // lane's entry of the weighted row g = i*N2 + r of [Q^1/2 G | Q^1/2 Phi]
+  auto rowval = [&](int g) __attribute__((always_inline)) -> double {
+    const int i = g / N2, r = g - i * N2;
     const double di = fabs(dl[i]);
     const double sqi = sc.wsq ? di : sqrt(di);
-    const int n1 = sc.n1[i];
-    const double* stp = sstep + i * nu * sc.tlen + gn * sc.tlen;
-    const double* prow = sc.phi + (long long)(i * sc.n2max) * nx + (lane - M);
-    double wnext = 0.0;
+    double v = 0.0;
     if (lane < M) {
-      const int tt = n1 - gc;
-      wnext = tt >= 0 ? stp[tt] : 0.0;
+      const int tt = sc.n1[i] + r - gc;
+      v = tt >= 0 ? sstep[(i * nu + gn) * sc.tlen + tt] : 0.0;
     } else if (lane < ncol) {
-      wnext = prow[0];
+      v = sc.phi[(long long)(i * sc.n2max + r) * nx + (lane - M)];
     }
-    for (int r = 0; r < N2; ++r) {
-      double w = wnext * sqi;
-      if (r + 1 < N2) {  // prefetch the next row
-        if (lane < M) {
-          const int tt = n1 + r + 1 - gc;
-          wnext = tt >= 0 ? stp[tt] : 0.0;
-        } else if (lane < ncol) {
-          wnext = prow[(long long)(r + 1) * nx];
-        }
-      }
+    return v * sqi;
+  };
+  // Givens rotation of row w against R's row k (decided by lane k, uniform); identity when the
+  // row's entry is already zero.  1/rho by v_rsq_f64 and two Newton steps.
+  auto rotate = [&](double& w, int k) __attribute__((always_inline)) {
+    const double b = bcast(w, k);
+    const double a = bcast(rcol[k], k);
+    const double x = a * a + b * b;
+    double ri = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    ri = ri * fma(-h * ri, ri, 1.5);
+    ri = ri * fma(-h * ri, ri, 1.5);
+    const bool nz = b != 0.0;
+    const double cs = nz ? a * ri : 1.0, sn = nz ? b * ri : 0.0;
+    const double rk = rcol[k];
+    rcol[k] = cs * rk + sn * w;
+    w = -sn * rk + cs * w;
+  };
+  // two rows in flight, skewed by one column: row g+1 meets R's row k after row g has
+  // (independent latency chains interleave)
+  const int P = my * N2;
+  int g = 0;
+  double n0 = P > 0 ? rowval(0) : 0.0, n1v = P > 1 ? rowval(1) : 0.0;  // prefetched pair
+  for (; g + 1 < P; g += 2) {
+    double w0 = n0, w1 = n1v;
+    if (g + 2 < P) n0 = rowval(g + 2);
+    if (g + 3 < P) n1v = rowval(g + 3);
 #pragma unroll
-      for (int k = 0; k < MAXM; ++k) {
-        if (k < M) {
-          const double b = bcast(w, k);
-          if (b != 0.0) {
-            const double a = bcast(rcol[k], k);
-            const double rinv = 1.0 / sqrt(a * a + b * b);
-            const double cs = a * rinv, sn = b * rinv;
-            const double rk = rcol[k];
-            rcol[k] = cs * rk + sn * w;
-            w = -sn * rk + cs * w;
-          }
-        }
-      }
+    for (int k = 0; k <= MAXM; ++k) {
+      if (k < M) rotate(w0, k);
+      if (k >= 1 && k - 1 < M) rotate(w1, k - 1);
     }
+  }
+  if (g < P) {
+    double w0 = n0;
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+      if (k < M) rotate(w0, k);
   }
   // R (upper) to LDS scratch (row-major) in the step-table region; singular R -> status
   double* sR = sstep;
@@ -890,6 +902,21 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   const double* ea = spla + ee * sc.pl_maxa;
   double* eyh = syeh + lane * kYeHist;
   const double* eur = sur + (ecopy * nin + ej) * kURing;
+  // register-resident per-lane state (regpath): plant entry taps / denominator / output history,
+  // output y(t-1) and its backward differences, MV past-control register
+  double bt[kRegB], at[kRegA], yh[kRegA], yd[kRegY], duh[kRegDu];
+#pragma unroll
+  for (int k = 0; k < kRegB; ++k) bt[k] = (is_entry && k < e_nb - e_off) ? eb[e_off + k] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kRegA; ++k) {
+    at[k] = (is_entry && k + 1 < e_na) ? ea[k + 1] : 0.0;
+    yh[k] = 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kRegY; ++k) yd[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < kRegDu; ++k) duh[k] = 0.0;
+  const bool regpath = sc.regpath != 0;
   // prefetched per-output signals
   double r_t = 0.0, yr_t = 0.0;
   if (lane < my) {
@@ -918,11 +945,24 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     if (is_entry) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
-      double a0 = 0.0, a1 = 0.0;
-      for (int l = e_off; l < e_nb; ++l) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
-      for (int l = 1; l < e_na; ++l) a1 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
-      const double acc = a0 + a1;
-      eyh[t & (kYeHist - 1)] = acc;
+      double acc;
+      if (regpath) {
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < kRegB; ++k) a0 += bt[k] * eur[(t - e_off - k) & (kURing - 1)];
+#pragma unroll
+        for (int k = 0; k < kRegA; ++k) a1 -= at[k] * yh[k];
+        acc = a0 + a1;
+#pragma unroll
+        for (int k = kRegA - 1; k > 0; --k) yh[k] = yh[k - 1];
+        yh[0] = acc;
+      } else {
+        double a0 = 0.0, a1 = 0.0;
+        for (int l = e_off; l < e_nb; ++l) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
+        for (int l = 1; l < e_na; ++l) a1 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
+        acc = a0 + a1;
+        eyh[t & (kYeHist - 1)] = acc;
+      }
       sye[lane] = acc;
     }
     lds_sync();
@@ -932,15 +972,30 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
-      double cur = y, prev = syprev[i];
-      for (int k = 1; k < nyh_i; ++k) {
-        const double old = sx[yoff_i + k];
-        const double nk = cur - prev;
-        sx[yoff_i + k] = nk;
-        cur = nk;
-        prev = old;
+      if (regpath) {  // yd = [y(t-1), nabla y(t-1), ...] in registers
+        double cur = y, prev = yd[0];
+#pragma unroll
+        for (int k = 1; k < kRegY; ++k) {
+          if (k < nyh_i) {
+            const double nk = cur - prev;
+            prev = yd[k];
+            yd[k] = nk;
+            cur = nk;
+            sx[yoff_i + k] = nk;
+          }
+        }
+        yd[0] = y;
+      } else {
+        double cur = y, prev = syprev[i];
+        for (int k = 1; k < nyh_i; ++k) {
+          const double old = sx[yoff_i + k];
+          const double nk = cur - prev;
+          sx[yoff_i + k] = nk;
+          cur = nk;
+          prev = old;
+        }
+        syprev[i] = y;
       }
-      syprev[i] = y;
       sx[yoff_i] = y - r_t;
       const double e1 = y - yr_t;
       j1 += e1 * e1;
@@ -962,8 +1017,17 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
-      for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
-      sx[upoff_n] = du;
+      if (regpath) {  // past-control register in registers, written out whole
+#pragma unroll
+        for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
+        duh[0] = du;
+#pragma unroll
+        for (int k = 0; k < kRegDu; ++k)
+          if (k < dum_n) sx[upoff_n + k] = duh[k];
+      } else {
+        for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
+        sx[upoff_n] = du;
+      }
       sur[n * kURing + (t & (kURing - 1))] = un;
       if (o.want_traj) {
         if (out.u) out.u[(sim * nu + n) * nit + t] = un;

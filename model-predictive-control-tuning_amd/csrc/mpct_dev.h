@@ -11,6 +11,11 @@ constexpr int kURing = 32;     // plant input history ring (power of two)
 constexpr int kMaxTaps = 16;   // longest plant numerator incl. delay (z^-1 taps)
 constexpr int kYeHist = 8;     // plant entry output history ring (power of two)
 constexpr int kMaxDum = 16;    // longest past-control register per MV (deltaUFree cp)
+// register-resident per-lane state (DevScenario::regpath; larger scenarios use the LDS path)
+constexpr int kRegB = 4;       // nonzero numerator taps per plant entry
+constexpr int kRegA = 4;       // denominator coefficients a_1.. per plant entry
+constexpr int kRegDu = 8;      // past-control register length per MV
+constexpr int kRegY = 6;       // y history (difference basis) length per output
 constexpr int kWave = 64;
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
@@ -29,6 +34,7 @@ struct DevScenario {
   int ink0;                 // VNS inK, 0-based
   int ne;                   // plant entries my*nin
   int pl_maxb, pl_maxa;     // longest plant numerator (incl. delay) / denominator
+  int regpath;              // every per-lane history / coefficient set fits the kReg* caps
   // tables (device pointers into one allocation)
   const double* step;   // [my][nu][tlen]   model step responses s_ij(t), t = 0..tlen-1
   const double* phi;    // [my*n2max][nx]   free response rows (Diophantine F | deltaUFree Hp)

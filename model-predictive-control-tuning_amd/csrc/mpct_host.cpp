@@ -429,6 +429,13 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.ne = s->ne;
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
+  {
+    bool rp = s->pl_maxa - 1 <= kRegA;
+    for (int e = 0; e < s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
+    for (int n = 0; n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
+    for (int i = 0; i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
+    ds.regpath = rp ? 1 : 0;
+  }
   ds.step = reinterpret_cast<const double*>(b + o_step);
   ds.phi = reinterpret_cast<const double*>(b + o_phi);
   ds.n1 = reinterpret_cast<const int*>(b + o_n1);
