@@ -125,6 +125,20 @@ __device__ __forceinline__ void wave_argmin64(double& v, int& id) {
   }
 }
 
+// sum over the four 16-lane rows (lanes l, l+16, l+32, l+48), result in every row:
+// v_permlane16_swap then v_permlane32_swap (gfx950), no LDS round trip
+__device__ __forceinline__ double row4_sum(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
+  lo = __double2loint(a);
+  hi = __double2hiint(a);
+  auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
+}
+
 // reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
 template <int MAXM>
 __device__ __forceinline__ double qsum(double v) {
@@ -832,7 +846,25 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   // unconstrained minimiser dU = A x, then the QP; result in sxc
   auto solve_step = [&]() __attribute__((always_inline)) {
     double xu = 0.0;
-    if (lane < M) {
+    if constexpr (MAXM <= 16) {
+      // the four 16-lane rows split A's column pairs; row m of A on lanes m, m+16, m+32, m+48
+      const int m = lane & 15, grp = lane >> 4;
+      const int npair = nxp / 2, per = (npair + 3) >> 2;
+      const int p0 = grp * per, p1 = min(npair, p0 + per);
+      double a0 = 0.0, a1 = 0.0;
+      if (m < M) {
+        const double2* arow = reinterpret_cast<const double2*>(sA + m * nxp);
+        const double2* xv = reinterpret_cast<const double2*>(sx);
+        for (int q2 = p0; q2 < p1; ++q2) {
+          const double2 av = arow[q2], xa = xv[q2];
+          a0 += av.x * xa.x;
+          a1 += av.y * xa.y;
+        }
+      }
+      xu = row4_sum(a0 + a1);
+      if (lane < M) sxc[lane] = xu;
+      if (lane >= M) xu = 0.0;
+    } else if (lane < M) {
       // 16-byte LDS reads: two A entries of this row and two x entries per load
       const double2* arow = reinterpret_cast<const double2*>(sA + lane * nxp);
       const double2* xv = reinterpret_cast<const double2*>(sx);
