@@ -718,105 +718,112 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   lds_sync();
 
   // QR of W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens rotations carrying V = [Q^1/2 Phi; 0]
-  // (lane l owns column l of [R | T]; rotation k decided by lane k, broadcast with v_readlane).
-  const int ncol = M + nx;  // <= 64 (checked on the host)
+  // (lane l < M owns column l of R, lane l >= M a column of T = Q1'V; rotation k decided by lane
+  // k, broadcast with v_readlane).  When M + nx > 64 the V columns are processed in passes of
+  // 64 - M; every pass recomputes the same rotations (bitwise identical R), so T is exact.
+  const int vper = kWave - M;  // V columns per pass (host guarantees M < 64)
+  const int npass = (nx + vper - 1) / vper;
   double rcol[MAXM];
-  {
-    double wl0 = 0.0;
-    if (lane < M) {
-      const double ln = fabs(lm[lane / Nu]);
-      wl0 = sc.wsq ? ln : sqrt(ln);
-    }
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? wl0 : 0.0;
-  }
   int gn = 0, gc = 0;
   if (lane < M) {
     gn = lane / Nu;
     gc = lane - gn * Nu;
   }
-  // lane's entry of the weighted row g = i*N2 + r of [Q^1/2 G | Q^1/2 Phi]
-  auto rowval = [&](int g) __attribute__((always_inline)) -> double {
-    const int i = g / N2, r = g - i * N2;
-    const double di = fabs(dl[i]);
-    const double sqi = sc.wsq ? di : sqrt(di);
-    double v = 0.0;
-    if (lane < M) {
-      const int tt = sc.n1[i] + r - gc;
-      v = tt >= 0 ? sstep[(i * nu + gn) * sc.tlen + tt] : 0.0;
-    } else if (lane < ncol) {
-      v = sc.phi[(long long)(i * sc.n2max + r) * nx + (lane - M)];
+  double* sR = lds + L.jt;  // R (upper, row-major) parks in J's region until the QP starts
+  for (int pass = 0; pass < npass; ++pass) {
+    const int vc = pass * vper + (lane - M);  // this lane's V column in this pass
+    const bool vlane = lane >= M && vc < nx;
+    {
+      double wl0 = 0.0;
+      if (lane < M) {
+        const double ln = fabs(lm[lane / Nu]);
+        wl0 = sc.wsq ? ln : sqrt(ln);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? wl0 : 0.0;
     }
-    return v * sqi;
-  };
-  // Givens rotation of row w against R's row k (decided by lane k, uniform); identity when the
-  // row's entry is already zero.  1/rho by v_rsq_f64 and two Newton steps.
-  auto rotate = [&](double& w, int k) __attribute__((always_inline)) {
-    const double b = bcast(w, k);
-    const double a = bcast(rcol[k], k);
-    const double x = a * a + b * b;
-    double ri = __builtin_amdgcn_rsq(x);
-    const double h = 0.5 * x;
-    ri = ri * fma(-h * ri, ri, 1.5);
-    ri = ri * fma(-h * ri, ri, 1.5);
-    const bool nz = b != 0.0;
-    const double cs = nz ? a * ri : 1.0, sn = nz ? b * ri : 0.0;
-    const double rk = rcol[k];
-    rcol[k] = cs * rk + sn * w;
-    w = -sn * rk + cs * w;
-  };
-  // two rows in flight, skewed by one column: row g+1 meets R's row k after row g has
-  // (independent latency chains interleave)
-  const int P = my * N2;
-  int g = 0;
-  double n0 = P > 0 ? rowval(0) : 0.0, n1v = P > 1 ? rowval(1) : 0.0;  // prefetched pair
-  for (; g + 1 < P; g += 2) {
-    double w0 = n0, w1 = n1v;
-    if (g + 2 < P) n0 = rowval(g + 2);
-    if (g + 3 < P) n1v = rowval(g + 3);
+    // lane's entry of the weighted row g = i*N2 + r of [Q^1/2 G | Q^1/2 Phi]
+    auto rowval = [&](int g) __attribute__((always_inline)) -> double {
+      const int i = g / N2, r = g - i * N2;
+      const double di = fabs(dl[i]);
+      const double sqi = sc.wsq ? di : sqrt(di);
+      double v = 0.0;
+      if (lane < M) {
+        const int tt = sc.n1[i] + r - gc;
+        v = tt >= 0 ? sstep[(i * nu + gn) * sc.tlen + tt] : 0.0;
+      } else if (vlane) {
+        v = sc.phi[(long long)(i * sc.n2max + r) * nx + vc];
+      }
+      return v * sqi;
+    };
+    // Givens rotation of row w against R's row k (decided by lane k, uniform); identity when
+    // the row's entry is already zero.  1/rho by v_rsq_f64 and two Newton steps.
+    auto rotate = [&](double& w, int k) __attribute__((always_inline)) {
+      const double b = bcast(w, k);
+      const double a = bcast(rcol[k], k);
+      const double x = a * a + b * b;
+      double ri = __builtin_amdgcn_rsq(x);
+      const double h = 0.5 * x;
+      ri = ri * fma(-h * ri, ri, 1.5);
+      ri = ri * fma(-h * ri, ri, 1.5);
+      const bool nz = b != 0.0;
+      const double cs = nz ? a * ri : 1.0, sn = nz ? b * ri : 0.0;
+      const double rk = rcol[k];
+      rcol[k] = cs * rk + sn * w;
+      w = -sn * rk + cs * w;
+    };
+    // two rows in flight, skewed by one column (independent latency chains interleave)
+    const int P = my * N2;
+    int g = 0;
+    double n0 = P > 0 ? rowval(0) : 0.0, n1v = P > 1 ? rowval(1) : 0.0;  // prefetched pair
+    for (; g + 1 < P; g += 2) {
+      double w0 = n0, w1 = n1v;
+      if (g + 2 < P) n0 = rowval(g + 2);
+      if (g + 3 < P) n1v = rowval(g + 3);
 #pragma unroll
-    for (int k = 0; k <= MAXM; ++k) {
-      if (k < M) rotate(w0, k);
-      if (k >= 1 && k - 1 < M) rotate(w1, k - 1);
-    }
-  }
-  if (g < P) {
-    double w0 = n0;
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k)
-      if (k < M) rotate(w0, k);
-  }
-  // R (upper) to LDS scratch (row-major) in the step-table region; singular R -> status
-  double* sR = sstep;
-  lds_sync();
-  if (lane < M) {
-#pragma unroll
-    for (int k = 0; k < MAXM; ++k)
-      if (k < M) sR[k * M + lane] = rcol[k];
-  }
-  lds_sync();
-  bool spd = true;
-  for (int k = 0; k < M; ++k)
-    if (!(sR[k * M + k] > 0.0)) spd = false;
-  if (!spd) {
-    write_nan(MPCT_ST_NONFINITE_);
-    return;
-  }
-  // A = -R^-1 T (lanes M..M+nx-1 solve for their own column), column-major [s][m]
-  if (lane >= M && lane < ncol) {
-#pragma unroll
-    for (int kk = MAXM - 1; kk >= 0; --kk) {
-      if (kk < M) {
-        double a = rcol[kk];
-#pragma unroll
-        for (int j = 0; j < MAXM; ++j)
-          if (j > kk && j < M) a -= sR[kk * M + j] * rcol[j];
-        rcol[kk] = a / sR[kk * M + kk];
+      for (int k = 0; k <= MAXM; ++k) {
+        if (k < M) rotate(w0, k);
+        if (k >= 1 && k - 1 < M) rotate(w1, k - 1);
       }
     }
+    if (g < P) {
+      double w0 = n0;
 #pragma unroll
-    for (int m = 0; m < MAXM; ++m)
-      if (m < M) sA[m * nxp + (lane - M)] = -rcol[m];
+      for (int k = 0; k < MAXM; ++k)
+        if (k < M) rotate(w0, k);
+    }
+    if (pass == 0) {  // R to LDS; singular R -> status
+      lds_sync();
+      if (lane < M) {
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+          if (k < M) sR[k * M + lane] = rcol[k];
+      }
+      lds_sync();
+      bool spd = true;
+      for (int k = 0; k < M; ++k)
+        if (!(sR[k * M + k] > 0.0)) spd = false;
+      if (!spd) {
+        write_nan(MPCT_ST_NONFINITE_);
+        return;
+      }
+    }
+    // A = -R^-1 T: V lanes solve for their own column, stored row-major A[m][vc]
+    if (vlane) {
+#pragma unroll
+      for (int kk = MAXM - 1; kk >= 0; --kk) {
+        if (kk < M) {
+          double a = rcol[kk];
+#pragma unroll
+          for (int j = 0; j < MAXM; ++j)
+            if (j > kk && j < M) a -= sR[kk * M + j] * rcol[j];
+          rcol[kk] = a / sR[kk * M + kk];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MAXM; ++m)
+        if (m < M) sA[m * nxp + vc] = -rcol[m];
+    }
   }
   if (lane < M && nxp > nx) sA[lane * nxp + nx] = 0.0;  // pad column
   // R^-1 (upper, row-major): lane j solves R x = e_j in its own LDS column (zeros below)

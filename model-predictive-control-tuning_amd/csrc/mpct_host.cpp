@@ -185,9 +185,9 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     delete s;
     return fail(MPCT_ERANGE, "free-response state too large");
   }
-  if (nu * s->numax + s->nx > kWave) {
+  if (nu * s->numax > kWave - 1) {
     delete s;
-    return fail(MPCT_ERANGE, "nu*nu_max + free-response state must fit one wavefront (<= 64 columns)");
+    return fail(MPCT_ERANGE, "nu*nu_max must be < 64 (one QP row per lane)");
   }
   // ---- Diophantine + deltaUFree per output (window rows j = n1_i .. n1_i + N - 1)
   s->phi.assign((size_t)my * N * s->nx, 0.0);

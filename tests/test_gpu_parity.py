@@ -170,3 +170,29 @@ def test_status_edges(env):
     empty = eval_batch(sc, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 3)),
                        np.zeros((0, 3)), env["r"][None])
     assert empty.J1.shape == (0, 3)
+
+
+def test_vns_search_ranges(built, has_gpu):
+    """MPCTuning.m:163 (nbp=7, nbc=4): N2 up to 127 and Nu up to 15, i.e. M = 45 QP rows and
+    M + nx = 80 > 64 columns in the prologue QR (multi-pass) -- against the C port."""
+    if not has_gpu:
+        pytest.skip("no GPU")
+    from mpct.engine import eval_batch
+    from mpct.scenarios import shell3x3
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3
+
+    sc, r, yref = shell3x3(n2_max=127, nu_max=15)
+    osc, orr, oyref, _ = o_shell3x3()
+    cp = CPort(osc, 127, 500, oyref)
+    rng = np.random.default_rng(11)
+    N2 = np.array([127, 127, 64, 16, 100, 33, 90, 127], dtype=np.int32)
+    Nu = np.array([15, 2, 15, 15, 7, 12, 1, 10], dtype=np.int32)
+    d = 10.0 ** rng.uniform(-3, 0, (8, 3))
+    l = 10.0 ** rng.uniform(-4, -1, (8, 3))
+    res = eval_batch(sc, N2, Nu, d, l, r[None], open_loop=True, want_traj=True)
+    ref = cp.eval(N2, Nu, d, l, orr[None], open_loop=True, want_traj=True)
+    assert np.all(res.status == 0) and np.all(ref["status"] == 0)
+    assert _rel(res.J1, ref["J1"]) < COST_RTOL
+    assert _trel(res.u, ref["u"]) < TRAJ_RTOL
+    assert _trel(res.uopt, ref["uopt"]) < TRAJ_RTOL
