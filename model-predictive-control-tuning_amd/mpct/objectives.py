@@ -34,7 +34,7 @@ def gam_fun(sc, X, N, Nu, Xsp, ov_weights=None):
     return res.J1, res
 
 
-def vns_objective(sc, N2, Nu, delta, lam, inK=10):
+def vns_objective(sc, N2, Nu, delta, lam, inK=10, device=-1):
     """F = sum(j21 + j22) + N(1) + sum(Jnu) (VNS2.m:195) for C candidates (square plant: my
     simulations per candidate, output i / MV i taken from simulation i, VNS2.m:148-165).
     Returns (F (C,), j21 (C,my), j22 (C,my), Jnu (C,nu), EvalResult)."""
@@ -43,7 +43,7 @@ def vns_objective(sc, N2, Nu, delta, lam, inK=10):
     N2 = np.atleast_1d(N2).astype(np.int32)
     Cn = N2.size
     refs = vns_step_refs(sc.my, sc.nit, inK)
-    res = eval_batch(sc, N2, Nu, delta, lam, refs, open_loop=True)
+    res = eval_batch(sc, N2, Nu, delta, lam, refs, open_loop=True, device=device)
     idx = np.arange(sc.my)
     j21 = res.j21.reshape(Cn, sc.my, sc.my)[:, idx, idx]
     j22 = res.j22.reshape(Cn, sc.my, sc.my)[:, idx, idx]

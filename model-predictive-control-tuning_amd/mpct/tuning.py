@@ -1,0 +1,422 @@
+"""The tuning loop around the batched closed-loop engine: MPCTuning's Par, the VNS horizon search,
+the GAM weight search and their alternation, and the Tuning_Parameters record.
+
+  de2bi / bits_of            Communications-toolbox de2bi as MPCTuning.m:285 / VNS2.m:210-215 use it
+  TuningPar                  Par of MPCTuning.m:307-340 (bit weights, initial horizons, bounds, ...)
+  vns2(par, evaluate, fv)    VNS2.m:1-292, control flow kept line by line (orders {1, 3} only, the
+                             ii increment sits inside the tt loop, first improvement, restarts)
+  vns2_batched(...)          the same search, every neighbour evaluation served from batches
+                             scored on the GPU (speculative replay, identical decisions)
+  gam_fgoalattain(...)       GAM_fun.m + MPC_TFob.m:61-67: goal attainment on J1 (restated)
+  mpc_tfob(...)              MPC_TFob.m:28-143: GAM / VNS alternation and its quirks
+  save_tuning_parameters     MPCTuning.m:374-381 record (MAT v5 via scipy.io.savemat, or JSON)
+
+The evaluators are callables, so the search logic is the same whether a neighbour is scored by
+the HIP engine (mpct.engine, the product path) or by a checker in tests.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .objectives import precon
+
+
+# --------------------------------------------------------------------------------------------
+def de2bi(x: int, n: int) -> list:
+    """de2bi(x, n): n bits, least significant first (MATLAB's default 'right-msb' ordering)."""
+    return [(int(x) >> k) & 1 for k in range(n)]
+
+
+def bits_of(x: int, n: int) -> list:
+    """flip(de2bi(x, n)): most significant bit first, the layout of Xv1 / Xv2 rows."""
+    return de2bi(x, n)[::-1]
+
+
+def bit_weights(nbp: int, nbc: int) -> np.ndarray:
+    """Fc of MPCTuning.m:270-278: [2^(nbp-1) .. 1, 2^(nbc-1) .. 1]."""
+    return np.array([2 ** i for i in range(nbp - 1, -1, -1)] + [2 ** i for i in range(nbc - 1, -1, -1)],
+                    dtype=np.int64)
+
+
+@dataclass
+class TuningPar:
+    """MPCTuning.m:264-340.  my outputs, ny MVs (the reference's Par.ny / Par.nu naming is
+    swapped, MPCTuning.m:307-308; here my = outputs, ny = inputs)."""
+
+    my: int
+    ny: int
+    nbp: int = 7
+    nbc: int = 4
+    dmin: np.ndarray = None         # minimal delay per output (MPCTuning.m:257-262)
+    w: np.ndarray = None            # GAM weights (Pareto), Shell3x3.m:161
+    q0: np.ndarray = None           # initial OV weights (mpcobj.Weights.OV)
+    w0: np.ndarray = None           # initial MV-rate weights (mpcobj.Weights.MVRate)
+    nit: int = 500
+    Fc: np.ndarray = field(default=None)
+    N: np.ndarray = field(default=None)
+    Nu: np.ndarray = field(default=None)
+    Xv1: list = field(default=None)
+    Xv2: list = field(default=None)
+    delta: np.ndarray = field(default=None)
+    lam: np.ndarray = field(default=None)
+    x0: np.ndarray = field(default=None)
+    lb1: np.ndarray = field(default=None)
+    ov_zero: np.ndarray = field(default=None)   # OV weights the user set to 0 (band mode)
+
+    def __post_init__(self):
+        if self.nbp < self.nbc:            # MPCTuning.m:138-140
+            self.nbp = self.nbc
+        self.Fc = bit_weights(self.nbp, self.nbc)
+        Hp, Hc = 2 ** self.nbp - 1, 2 ** self.nbc - 1     # MPCTuning.m:283-285
+        self.Xv1 = bits_of(Hp, self.nbp)
+        self.Xv2 = [bits_of(Hc, self.nbc) for _ in range(self.ny)]   # MPC_TFob.m:46-50
+        self.N = np.full(self.my, Hp, dtype=np.int64)                # MPCTuning.m:288
+        self.Nu = np.full(self.ny, 2, dtype=np.int64)                # MPCTuning.m:289
+        self.delta = np.ones(self.my)                                # MPCTuning.m:265-266
+        self.lam = np.ones(self.ny)
+        q0 = np.ones(self.my) if self.q0 is None else np.asarray(self.q0, dtype=float)
+        w0 = np.ones(self.ny) if self.w0 is None else np.asarray(self.w0, dtype=float)
+        self.ov_zero = q0 == 0
+        self.x0 = np.concatenate([q0, w0])                           # MPCTuning.m:300
+        self.lb1 = np.full(self.my + self.ny, 1e-5)                  # MPCTuning.m:302
+        self.dmin = np.zeros(self.my, dtype=np.int64) if self.dmin is None else np.asarray(self.dmin)
+        self.w = np.ones(self.my) if self.w is None else np.asarray(self.w, dtype=float)
+
+
+# --------------------------------------------------------------------------------------------
+def vns2(par: TuningPar, evaluate, fv: float):
+    """VNS2.m:1-292 with the MATLAB control flow kept line by line.
+
+    evaluate(N, Nu) -> F (VNS2.m:147-195 for the neighbour, max(N)/max(Nu) horizons).
+    fv is the global Fv (best cost so far, MPCTuning.m:292).  Returns
+    (N, Nu, Xv1, Xv2, Fvns, fv, n_evals).  A failed simulation (NaN F) never improves.
+    """
+    my, ny = par.my, par.ny
+    Fc = [int(v) for v in par.Fc]
+    nbp = par.nbp
+    Fc1, Fc2 = Fc[:nbp], Fc[nbp:]
+    Nt1, Nt2 = len(Fc1), len(Fc2)
+    Xv1 = list(par.Xv1)
+    Xv2 = [list(r) for r in par.Xv2]
+    N = [int(v) for v in par.N]
+    Nu = [int(v) for v in par.Nu]
+    Nu1 = list(Nu)
+    dmin = [int(v) for v in par.dmin]
+    dot = lambda c, x: sum(a * b for a, b in zip(c, x))          # noqa: E731
+    n_evals = 0
+
+    ii = 1
+    while ii <= 3:                                   # VNS2.m:89
+        Order = ii
+        tt = 1
+        m = 1
+        Hpc = my
+        H = 1
+        while tt <= 2:                               # VNS2.m:98 (ii advances inside: orders 1, 3)
+            while H <= Hpc:
+                if tt == 1:
+                    Nt, X3, Fc3 = Nt1, [None] + list(Xv1), Fc1
+                else:
+                    Nt, X3, Fc3 = Nt2, [None] + list(Xv2[H - 1]), Fc2
+                Ix = [None, Nt]                      # 1-based like the reference
+                for i in range(2, Order + 1):
+                    Ix.append(Ix[i - 1] - 1)
+                while Ix[1] >= 1 and tt != 0:        # VNS2.m:114
+                    for t in range(1, Order):        # static indices (VNS2.m:116-120)
+                        if 0 < Ix[t] <= Nt:
+                            X3[Ix[t]] = 1 - X3[Ix[t]]
+                    while Ix[-1] >= 1:               # VNS2.m:122
+                        X3[Ix[-1]] = 1 - X3[Ix[-1]]
+                        if tt == 1:
+                            N[:] = [dot(Fc3, X3[1:])] * my
+                        else:
+                            Nu[H - 1] = dot(Fc3, X3[1:])
+                            Nu1[H - 1] = dot(Fc2, Xv2[H - 1])
+                        if (not precon(N, Nu) or not precon(N, Nu1) or any(n <= d for n, d in zip(N, dmin))
+                                or any(u <= 1 for u in Nu)):      # VNS2.m:135
+                            X3[Ix[-1]] = 1 - X3[Ix[-1]]
+                            if tt == 1:
+                                N[:] = [dot(Fc3, X3[1:])] * my
+                            else:
+                                Nu[H - 1] = dot(Fc3, X3[1:])
+                        else:
+                            F = evaluate(tuple(N), tuple(Nu))
+                            n_evals += 1
+                            if F < fv:                            # VNS2.m:198
+                                fv = F
+                                Ix[1] = Nt
+                                for i in range(2, Order + 1):
+                                    Ix[i] = Ix[i - 1] - 1
+                                Ix[-1] = -1
+                                Ix[1] = -1
+                                Xv1 = bits_of(N[0], len(Fc1))     # VNS2.m:210-215
+                                Xv2 = [bits_of(Nu[i], len(Fc2)) for i in range(ny)]
+                            else:                                 # discard the neighbour
+                                X3[Ix[-1]] = 1 - X3[Ix[-1]]
+                                if tt == 1:
+                                    N[:] = [dot(Fc3, X3[1:])] * my
+                                else:
+                                    Nu[H - 1] = dot(Fc3, X3[1:])
+                        Ix[-1] -= 1                               # VNS2.m:223
+                    X3 = [None] + (list(Xv1) if tt == 1 else list(Xv2[H - 1]))
+                    if Order == 1 and Ix[1] < 0:                  # VNS2.m:233-239
+                        Ix[1] = Nt
+                        pos = [1]
+                    else:
+                        pos = [2]
+                    while pos and pos[0] != 1:                    # VNS2.m:241-251
+                        pos = [k for k in range(1, len(Ix)) if Ix[k] == 0]
+                        if pos and pos[0] != 1:
+                            p0 = pos[0]
+                            Ix[p0 - 1] -= 1
+                            Ix[p0] = Ix[p0 - 1] - 1
+                        pos = [k for k in range(1, len(Ix)) if Ix[k] == 0]
+                    if not pos and Ix[1] != -1:                   # VNS2.m:255-259
+                        neg = [k for k in range(1, len(Ix)) if Ix[k] < 0]
+                        if neg:
+                            for j in range(neg[0], Order + 1):
+                                Ix[j] = Ix[j - 1] - 1
+                if tt == 0:
+                    H = Hpc
+                H += 1
+            H = 1
+            tt += 1
+            if m <= 1 or tt == 1:                    # VNS2.m:276-281
+                Hpc = my
+            if tt == 2:
+                Hpc = ny
+            ii += 1
+    N = [dot(Fc1, Xv1)] * my                         # VNS2.m:285-289
+    Nu = [dot(Fc2, Xv2[i]) for i in range(ny)]
+    return np.array(N), np.array(Nu), Xv1, Xv2, fv, fv, n_evals
+
+
+class _Miss(Exception):
+    pass
+
+
+def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512):
+    """vns2 with every neighbour scored in GPU batches and the SAME decisions as the sequential
+    search.  A speculative pass replays the search from the start with the scores known so far;
+    unknown neighbours are taken as non-improving and collected, then scored together in one
+    batch (batch_evaluate(list of (N, Nu)) -> list of F).  Replays repeat until a pass needs
+    nothing unknown; every decision of the final pass was taken on real scores, and speculated
+    neighbours never change the search state (a rejected neighbour is reverted), so the result
+    equals the sequential search's.  Returns vns2's tuple plus the number of batches."""
+    cache = {}
+    n_batches = 0
+    while True:
+        pending = []
+
+        def spec(N, Nu):
+            key = (N, Nu)
+            if key in cache:
+                return cache[key]
+            if key not in pending and len(pending) < max_batch:
+                pending.append(key)
+            return math.inf
+
+        out = vns2(par, spec, fv)
+        if not pending:
+            return out + (n_batches,)
+        scores = batch_evaluate(pending)
+        n_batches += 1
+        for key, F in zip(pending, scores):
+            cache[key] = float(F) if np.isfinite(F) else math.nan
+
+
+# --------------------------------------------------------------------------------------------
+def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_change: float = 0.5,
+                    max_iter: int = 400, ftol: float = 1e-3):
+    """GAM step of MPC_TFob.m:61-67: fgoalattain(@GAM_fun, x0, goal=0.001, weight=w, lb=1e-5,
+    EqualityGoalCount = numel(w)) -- restated as the goal-attainment problem
+        min gamma  s.t.  |J1_i(x) - goal| <= w_i * gamma,  x >= lb1
+    solved by SLSQP with forward-difference Jacobians whose step is at least DiffMinChange
+    (MPCTuning.m:88-91: 'DiffMinChange', 0.5); each Jacobian is ONE batch of my+ny+1 closed
+    loops.  batch_j1(X rows) -> J1 rows (GAM_fun.m:55-116 for each row).  MATLAB's SQP internals
+    are not public: parity with fgoalattain's iterate sequence is unpinned; the goal-attainment
+    formulation and options are the reference's.  Returns (x, attainfactor, last_J1, n_batches)."""
+    from scipy.optimize import minimize
+
+    my, ny = par.my, par.ny
+    n = my + ny
+    w = np.asarray(par.w, dtype=float)
+    cache = {}
+    nb = [0]
+    last = [None]
+
+    def evals(X):
+        keys = [tuple(np.round(x, 15)) for x in X]
+        todo = [i for i, k in enumerate(keys) if k not in cache]
+        if todo:
+            J = batch_j1(np.array([X[i] for i in todo]))
+            nb[0] += 1
+            for i, j in zip(todo, J):
+                cache[keys[i]] = np.asarray(j, dtype=float)
+        return [cache[k] for k in keys]
+
+    def fd_points(x):
+        h = np.maximum(diff_min_change, np.sqrt(np.finfo(float).eps) * np.abs(x))
+        return [x] + [x + h[k] * np.eye(n)[k] for k in range(n)], h
+
+    def jac_F(x):
+        pts, h = fd_points(x)
+        vals = evals(pts)
+        F0 = vals[0]
+        Jm = np.stack([(vals[k + 1] - F0) / h[k] for k in range(n)], axis=1)   # my x n
+        return F0, Jm
+
+    def F(x):
+        v = evals([x])[0]
+        last[0] = v
+        return v
+
+    x0 = np.maximum(np.asarray(par.x0, dtype=float), par.lb1)
+    F0 = F(x0)
+    g0 = float(np.max(np.abs(F0 - goal) / w))
+    z0 = np.concatenate([x0, [g0]])
+    cons = [
+        {"type": "ineq", "fun": lambda z: w * z[-1] - (F(z[:-1]) - goal),
+         "jac": lambda z: np.hstack([-jac_F(z[:-1])[1], w[:, None]])},
+        {"type": "ineq", "fun": lambda z: w * z[-1] + (F(z[:-1]) - goal),
+         "jac": lambda z: np.hstack([jac_F(z[:-1])[1], w[:, None]])},
+    ]
+    bounds = [(lb, None) for lb in par.lb1] + [(None, None)]
+    res = minimize(lambda z: z[-1], z0, jac=lambda z: np.eye(n + 1)[-1], method="SLSQP",
+                   constraints=cons, bounds=bounds, options={"maxiter": max_iter, "ftol": ftol})
+    x = np.maximum(res.x[:-1], par.lb1)
+    Fx = F(x)
+    attain = float(np.max(np.abs(Fx - goal) / w))
+    return x, attain, Fx, nb[0]
+
+
+# --------------------------------------------------------------------------------------------
+def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None):
+    """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
+    improve.  Quirks kept: Fgam = round(sum(F), 2) of the GAM cost (MPC_TFob.m:104, here at the
+    returned point); OV weights the user set to 0 stay 0 (:83-93); the returned delta/lambda are
+    the LAST GAM result, not the best (:134-135).  Returns (N, Nu, lam, delta, Fvns, Fvf, fv)."""
+    my = par.my
+    Fva, Fvf = 10e8, 1e15
+    hi = 0
+    delta = lam = None
+    Fvns = fv
+    while True:
+        x, attain, Fx, _ = gam_fgoalattain(par, batch_j1)
+        x = x.copy()
+        x[:my][par.ov_zero] = 0.0
+        par.x0 = x
+        delta = np.abs(x[:my])
+        lam = np.abs(x[my:])
+        Fgam = round(float(np.sum(Fx)), 2)
+        if log:
+            log("Fgam=%g; Delta=%s; Lambda=%s" % (Fgam, delta, lam))
+        if Fgam >= Fvf:
+            hi += 1
+        else:
+            Fvf = Fgam
+            par.lam, par.delta = lam, delta
+
+        def bv(keys, _d=par.delta, _l=par.lam):
+            return batch_vns(keys, _d, _l)
+
+        N, Nu, Xv1, Xv2, Fvns, fv, _, _ = vns2_batched(par, bv, fv)
+        if Fvns < Fva:
+            Fva = Fvns
+            par.N, par.Nu, par.Xv1, par.Xv2 = N, Nu, Xv1, Xv2
+        if log:
+            log("Fvns=%g; N=%s; Nu=%s" % (Fvns, par.N, par.Nu))
+        if hi > 0:
+            break
+    par.lam, par.delta = lam, delta
+    return par.N, par.Nu, par.lam, par.delta, Fvns, Fvf, fv
+
+
+# --------------------------------------------------------------------------------------------
+def save_tuning_parameters(path: str, N, Nu, delta, lam, scale: dict | None = None, date: str | None = None):
+    """MPCTuning.m:374-381 Tuning_Parameters {N, Nu, delta, lambda, scale.{L,R,Ru,Rv}, date}
+    (the mpc object itself is MATLAB-only and is not written).  '.mat' -> MAT v5 via scipy,
+    anything else -> JSON.  The struct reads back with the drivers' tuning=false path
+    (Shell3x3.m:169-185: Tuning_Parameters.N / .Nu / .delta / .lambda)."""
+    import datetime
+
+    rec = {"N": int(np.max(N)), "Nu": np.asarray(Nu, dtype=float).reshape(1, -1),
+           "delta": np.asarray(delta, dtype=float).reshape(1, -1),
+           "lambda": np.asarray(lam, dtype=float).reshape(1, -1),
+           "date": date or datetime.datetime.now().strftime("%d-%b-%Y %H:%M:%S")}
+    if scale is not None:
+        rec["scale"] = {k: np.asarray(v, dtype=float) for k, v in scale.items()}
+    if path.endswith(".mat"):
+        from scipy.io import savemat
+
+        savemat(path, {"Tuning_Parameters": rec})
+    else:
+        def conv(v):
+            if isinstance(v, dict):
+                return {k: conv(x) for k, x in v.items()}
+            if isinstance(v, np.ndarray):
+                return v.tolist()
+            return v
+
+        with open(path, "w") as f:
+            json.dump({"Tuning_Parameters": conv(rec)}, f, indent=1)
+    return rec
+
+
+# --------------------------------------------------------------------------------------------
+def engine_evaluators(sc, r, par: TuningPar, device: int = -1):
+    """Batched evaluators over the HIP engine (one eval_batch call per batch):
+      batch_j1(X rows)                 -> J1 rows  (GAM_fun.m:55-116 with Par.N / Par.Nu, which
+                                          closedloop_toolbox reduces with max, :36-40)
+      batch_vns(keys, delta, lambda)   -> F per (N, Nu) neighbour (VNS2.m:147-195: my step
+                                          simulations for square plants, F = sum(j21 + j22) +
+                                          N(1) + sum(Jnu)); failed simulations score NaN."""
+    from .engine import eval_batch
+    from .objectives import vns_objective
+
+    my, ny = par.my, par.ny
+
+    def batch_j1(X):
+        X = np.atleast_2d(np.asarray(X, dtype=float))
+        C = X.shape[0]
+        delta = np.abs(X[:, :my]).copy()
+        delta[:, par.ov_zero] = 0.0                   # GAM_fun.m:62-72
+        lam = np.abs(X[:, my:my + ny])
+        N2 = np.full(C, int(np.max(par.N)), dtype=np.int32)
+        Nu = np.full(C, int(np.max(par.Nu)), dtype=np.int32)
+        res = eval_batch(sc, N2, Nu, delta, lam, np.asarray(r)[None], device=device)
+        J1 = res.J1.copy()
+        J1[res.status != 0] = np.nan
+        return J1
+
+    def batch_vns(keys, delta, lam):
+        C = len(keys)
+        N2 = np.array([max(k[0]) for k in keys], dtype=np.int32)
+        Nu = np.array([max(k[1]) for k in keys], dtype=np.int32)
+        d = np.tile(np.asarray(delta, dtype=float), (C, 1))
+        l = np.tile(np.asarray(lam, dtype=float), (C, 1))
+        F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device)
+        ok = res.status.reshape(C, -1).max(axis=1) == 0
+        return np.where(ok, F, np.nan)
+
+    return batch_j1, batch_vns
+
+
+def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
+               device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None):
+    """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
+    scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
+    (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters."""
+    par = TuningPar(my=my, ny=ny, nbp=nbp, nbc=nbc, dmin=dmin, w=w, q0=q0, w0=w0, nit=sc.nit)
+    if sc.n2_max < 2 ** par.nbp - 1 or sc.nu_max < 2 ** par.nbc - 1:
+        raise ValueError("scenario horizons (n2_max=%d, nu_max=%d) must cover the bit ranges "
+                         "(%d, %d)" % (sc.n2_max, sc.nu_max, 2 ** par.nbp - 1, 2 ** par.nbc - 1))
+    batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device)
+    N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log)
+    if save_path:
+        save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
+    return N, Nu, delta, lam, np.array([Fvns, Fgam])

@@ -1,0 +1,171 @@
+"""CPU: the tuning loop around the engine (mpct.tuning) -- MPCTuning's bit encoding, the VNS2
+enumeration semantics (orders {1, 3}, first improvement, restarts), the batched speculative
+replay (identical decisions to the sequential search), the GAM goal-attainment restatement and
+the Tuning_Parameters record.  Neighbours are scored by synthetic functions or by the C port
+(oracle/cgpc.c) standing in for the GPU engine."""
+import math
+
+import numpy as np
+import pytest
+
+from mpct.tuning import (TuningPar, bit_weights, bits_of, de2bi, gam_fgoalattain, save_tuning_parameters,
+                         vns2, vns2_batched)
+
+
+def test_bits():
+    assert de2bi(5, 4) == [1, 0, 1, 0]           # least significant first (de2bi default)
+    assert bits_of(5, 4) == [0, 1, 0, 1]         # flip(de2bi(.)): Xv layout (MPCTuning.m:285)
+    assert bits_of(127, 7) == [1] * 7
+    np.testing.assert_array_equal(bit_weights(7, 4), [64, 32, 16, 8, 4, 2, 1, 8, 4, 2, 1])
+    p = TuningPar(my=3, ny=3, nbp=7, nbc=4)
+    np.testing.assert_array_equal(p.N, [127, 127, 127])      # MPCTuning.m:288-289
+    np.testing.assert_array_equal(p.Nu, [2, 2, 2])
+    assert p.Xv2 == [[1, 1, 1, 1]] * 3                        # MPC_TFob.m:46-50 (all ones)
+    assert TuningPar(my=1, ny=1, nbp=2, nbc=4).nbp == 4       # MPCTuning.m:138-140
+
+
+def test_vns2_enumeration_count():
+    """Never-improving search from MPCTuning's start (N = 127, Nu = [2 2 2], Xv2 = 15):
+    order 1: 3 x 7 (N search repeated my times) + 3 x 4 Nu flips (each rejected flip leaves
+    Nu(H) at the incumbent bits' value 15, VNS2.m:218-220); order 3: 3 x (C(7,3) - 1) N triples
+    (N = 127 - 112 = 15 fails PreCon against Nu = 15) + 3 x 3 Nu triples (Nu = 1 is invalid,
+    VNS2.m:135) = 144 evaluations."""
+    par = TuningPar(my=3, ny=3, nbp=7, nbc=4, dmin=np.array([6, 3, 0]))
+    seen = []
+
+    def ev(N, Nu):
+        seen.append((N, Nu))
+        return math.inf
+
+    N, Nu, Xv1, Xv2, Fvns, fv, n = vns2(par, ev, 1e30)
+    assert n == 144 == len(seen)
+    assert Fvns == 1e30
+    # every N neighbour of order 1 flips one bit of 127; order 3 flips three distinct bits
+    order1 = {k[0][0] for k in seen if k[1] == (2, 2, 2)}          # first pass: Nu still [2 2 2]
+    order3 = {k[0][0] for k in seen if k[1] == (15, 15, 15) and k[0][0] != 127}
+    assert order1 == {127 - 2 ** b for b in range(7)}
+    assert order3 == {127 - (2 ** a + 2 ** b + 2 ** c)
+                      for a in range(7) for b in range(a) for c in range(b)} - {15}
+    # the returned horizons come from the incumbent bits (quirk: Xv2 = 15 when nothing improved)
+    np.testing.assert_array_equal(N, [127] * 3)
+    np.testing.assert_array_equal(Nu, [15] * 3)
+
+
+def _synthetic(N, Nu):
+    return (N[0] - 37) ** 2 + sum((u - 5) ** 2 for u in Nu) + 0.5 * N[0] + 0.01 * sum(Nu)
+
+
+def test_vns2_batched_equals_sequential_synthetic():
+    par = TuningPar(my=3, ny=3, nbp=7, nbc=4, dmin=np.array([6, 3, 0]))
+    seq = vns2(par, _synthetic, 1e30)
+    calls = []
+
+    def batch(keys):
+        calls.append(len(keys))
+        return [_synthetic(*k) for k in keys]
+
+    bat = vns2_batched(par, batch, 1e30)
+    np.testing.assert_array_equal(seq[0], bat[0])
+    np.testing.assert_array_equal(seq[1], bat[1])
+    assert seq[2] == bat[2] and seq[3] == bat[3] and seq[4] == bat[4]
+    assert seq[6] == bat[6]                          # same number of scored neighbours
+    assert len(calls) == bat[7] and max(calls) <= 512
+    assert seq[4] < 1e30                             # the synthetic search does improve
+
+
+def test_vns2_first_improvement_restart():
+    """Hand-traced from VNS2.m (nbp = 4, nbc = 2, one output/input, F = |N - 5| + 0.1 Nu):
+    order 1 flips from index Nt = the least significant bit (VNS2.m:108) and restarts there after
+    every improvement (:198-215, 233-236): 15 -> 14 (better) -> 15 x, 12 (better) -> 13 x, 14 x,
+    8 (better) -> 9 x, 10 x, 12 x, 0 invalid.  The Nu search starts from Xv2 recomputed at the
+    first improvement (bits of Nu = 2): (8, 3) x.  Order 3 flips bits {4, 3} statically and then
+    bit 2 -> 15 x, bit 1 -> 3 (better): an improvement ends an order-3 block.  Nu has only 2 bits,
+    so its order-3 block is empty.  Result N = 3, F = 2.2."""
+    par = TuningPar(my=1, ny=1, nbp=4, nbc=2)
+    trace = []
+
+    def ev(N, Nu):
+        trace.append((N[0], Nu[0]))
+        return abs(N[0] - 5) + 0.1 * Nu[0]
+
+    N, Nu, _, _, F, _, n = vns2(par, ev, 1e30)
+    assert trace == [(14, 2), (15, 2), (12, 2), (13, 2), (14, 2), (8, 2), (9, 2), (10, 2), (12, 2),
+                     (8, 3), (15, 2), (3, 2)]
+    assert N[0] == 3 and Nu[0] == 2 and F == pytest.approx(2.2) and n == 12
+
+
+def test_gam_goal_attainment_synthetic():
+    """min gamma s.t. |J_i(x) - goal| <= w_i gamma, x >= 1e-5, forward differences with step
+    DiffMinChange = 0.5 (MPCTuning.m:88-91), Jacobian = one batch of n+1 points."""
+    par = TuningPar(my=2, ny=1, w=np.array([0.5, 0.5]))
+    par.x0 = np.array([2.0, 2.0, 2.0])
+    a = np.array([1.0, 3.0, 0.5])
+
+    def batch_j1(X):
+        X = np.atleast_2d(X)
+        J0 = (X[:, 0] - a[0]) ** 2 + 0.1 * X[:, 2] ** 2 + 1e-3
+        J1 = (X[:, 1] - a[1]) ** 2 + 0.1 * X[:, 2] ** 2 + 1e-3
+        return np.stack([J0, J1], axis=1)
+
+    F0 = batch_j1(par.x0)[0]
+    att0 = np.max(np.abs(F0 - 1e-3) / par.w)
+    x, att, Fx, nb = gam_fgoalattain(par, batch_j1)
+    assert np.all(x >= par.lb1)
+    assert att < 0.5 * att0
+    assert att == pytest.approx(np.max(np.abs(Fx - 1e-3) / par.w))
+    assert nb >= 2
+
+
+def test_tuning_parameters_roundtrip(tmp_path):
+    from scipy.io import loadmat
+
+    p = str(tmp_path / "Shell3x3_Tuning_test.mat")
+    save_tuning_parameters(p, [24, 24, 24], [6, 2, 2], [0.01, 0.004, 0.0008], [9e-5, 5e-4, 1.5e-3],
+                           scale={"L": np.eye(3), "R": np.eye(3)}, date="15-Oct-2026 12:00:00")
+    m = loadmat(p, squeeze_me=True, struct_as_record=False)["Tuning_Parameters"]
+    assert int(m.N) == 24
+    np.testing.assert_array_equal(np.atleast_1d(m.Nu), [6, 2, 2])
+    np.testing.assert_allclose(np.atleast_1d(m.delta), [0.01, 0.004, 0.0008])
+    np.testing.assert_allclose(m.scale.L, np.eye(3))
+    j = str(tmp_path / "t.json")
+    rec = save_tuning_parameters(j, [12], [4, 2, 2], [1, 1, 1], [1, 1, 1])
+    assert rec["N"] == 12
+
+
+def test_vns2_batched_equals_sequential_cport(built):
+    """The real Shell 3x3 VNS call (MPCTuning's start, fixture-tuned weights) scored by the C port:
+    the batched replay takes exactly the sequential search's decisions."""
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3, vns_step_refs
+
+    osc, r, yref, fx = shell3x3()
+    cp = CPort(osc, 127, 500, yref)
+    refs = np.asarray(vns_step_refs(3, 500))
+    delta, lam = np.asarray(fx["delta"]), np.asarray(fx["lambda"])
+    idx = np.arange(3)
+
+    def score(keys, threads):
+        C = len(keys)
+        N2 = np.array([max(k[0]) for k in keys], dtype=np.int32)
+        Nu = np.array([max(k[1]) for k in keys], dtype=np.int32)
+        res = cp.eval(N2, Nu, np.tile(delta, (C, 1)), np.tile(lam, (C, 1)), refs, open_loop=True,
+                      threads=threads)
+        j21 = res["j21"].reshape(C, 3, 3)[:, idx, idx]
+        j22 = res["j22"].reshape(C, 3, 3)[:, idx, idx]
+        jnu = res["Jnu"].reshape(C, 3, 3)[:, idx, idx]
+        return j21.sum(1) + j22.sum(1) + N2 + jnu.sum(1)
+
+    par = TuningPar(my=3, ny=3, nbp=7, nbc=4, dmin=np.array([6, 3, 0]))
+    bat = vns2_batched(par, lambda keys: score(keys, 8), 1e30)
+    cache = {}
+
+    def seq_eval(N, Nu):
+        if (N, Nu) not in cache:
+            cache[(N, Nu)] = float(score([(N, Nu)], 3)[0])
+        return cache[(N, Nu)]
+
+    seq = vns2(par, seq_eval, 1e30)
+    np.testing.assert_array_equal(seq[0], bat[0])
+    np.testing.assert_array_equal(seq[1], bat[1])
+    assert seq[4] == bat[4] and seq[6] == bat[6]
+    assert seq[4] < 1e30
