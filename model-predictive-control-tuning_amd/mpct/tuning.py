@@ -295,7 +295,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
 
 
 # --------------------------------------------------------------------------------------------
-def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None):
+def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400):
     """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
     improve.  Quirks kept: Fgam = round(sum(F), 2) of the GAM cost (MPC_TFob.m:104, here at the
     returned point); OV weights the user set to 0 stay 0 (:83-93); the returned delta/lambda are
@@ -306,7 +306,7 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None):
     delta = lam = None
     Fvns = fv
     while True:
-        x, attain, Fx, _ = gam_fgoalattain(par, batch_j1)
+        x, attain, Fx, _ = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter)
         x = x.copy()
         x[:my][par.ov_zero] = 0.0
         par.x0 = x
@@ -407,7 +407,8 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1):
 
 
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
-               device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None):
+               device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
+               gam_max_iter: int = 400):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters."""
@@ -416,7 +417,8 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
         raise ValueError("scenario horizons (n2_max=%d, nu_max=%d) must cover the bit ranges "
                          "(%d, %d)" % (sc.n2_max, sc.nu_max, 2 ** par.nbp - 1, 2 ** par.nbc - 1))
     batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device)
-    N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log)
+    N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
+                                                  gam_max_iter=gam_max_iter)
     if save_path:
         save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
     return N, Nu, delta, lam, np.array([Fvns, Fgam])
