@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 1
+#define MPCT_ABI_VERSION 2 /* 2: DTC-GPC predictor + plant-only disturbances; v1 descriptors accepted */
 
 /* error codes */
 #define MPCT_OK 0
@@ -94,6 +94,20 @@ typedef struct mpct_scenario_desc {
   const double* u_min;
   const double* u_max;
   const double* yref;
+  /* ---- abi_version >= 2 (ignored for version 1 descriptors) -------------------------------
+   * dtc      1: DTC-GPC (DTC_GPC_WW.m:126-164): the free response is driven by the predictor
+   *             yp = Gz*u + Fr*(y - Pz*u) (OptimalPredictor2.m:24-40) instead of the measured y.
+   *             The caller passes the model with its real delays (MatG window n1 = dmin+1),
+   *             dp = dnz = descompMPC delays minus dmin (deltaUFree.m / DTC_GPC_WW.m:91-93) and
+   *             the Diophantine window starts at d = 0 (DTC_GPC_WW.m:80).  Requires open_loop 0.
+   * filter   [my] Fr_i(z) (mimofilter.m / filtro_siso.m), delay 0; NULL -> Fr = 1
+   * nq       plant-only disturbance inputs: they drive the simulated plant through dist and are
+   *             never seen by the controller's model (DTC_GPC_WW.m:29-30 Pq, :128-129)
+   * dist     [my*nq] disturbance paths; their signals are the rows of eval's v: [nref][nd+nq][nit] */
+  int32_t dtc;
+  const mpct_dtf* filter;
+  int32_t nq;
+  const mpct_dtf* dist;
 } mpct_scenario_desc;
 
 typedef struct mpct_scenario mpct_scenario;
@@ -152,7 +166,7 @@ int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, double* buf, 
  *   delta[C*my], lambda[C*nu]   Weights.OV, Weights.MVRate (closedloop_toolbox.m:42-43)
  *   r[nref*my*nit]    reference sets (row signals; VNS passes one unit step per output,
  *                     VNS2.m:148-150; GAM passes Xsp)
- *   v[nref*nd*nit]    measured disturbances per reference set (may be NULL when nd == 0)  */
+ *   v[nref*(nd+nq)*nit] disturbance signals per reference set (NULL when nd + nq == 0)     */
 int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
                         const double* delta, const double* lambda, int32_t nref, const double* r,
                         const double* v, const mpct_opts* opts, mpct_result* out);

@@ -29,11 +29,15 @@
 namespace mpct {
 
 struct LdsLayout {
-  int rinv, jt, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, plb, pla, step, total;
+  int rinv, jt, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb, mza,
+      frb, fra, step, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, int ne, int my,
-                                                int tlen, int plb, int pla) {
+// LDS layout of one simulation; [x, plb) holds the state and every history (zeroed at start)
+__host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
+  const int nx = sc.nx, nu = sc.nu, nin = sc.nin, ne = sc.ne, my = sc.my;
+  const int nmz = sc.dtc ? 2 * my * nu : 0;  // DTC predictor model entries (Pz, Gz)
+  const int nfr = sc.dtc ? my : 0;           // DTC robustness filters
   LdsLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
@@ -51,9 +55,16 @@ __host__ __device__ inline LdsLayout lds_layout(int M, int nx, int nu, int nin, 
   L.ye = take(2 * ne);
   L.yeh = take(2 * ne * kYeHist);
   L.uring = take(2 * nin * kURing);
-  L.plb = take(ne * plb);
-  L.pla = take(ne * pla);
-  L.step = take(my * nu * tlen > M * M ? my * nu * tlen : M * M);  // prologue only
+  L.mzh = take(nmz * kYeHist);   // DTC: model entry output histories
+  L.smz = take(nmz);             // DTC: model entry outputs of the step
+  L.frh = take(nfr * 2 * kYeHist);  // DTC: filter input (eM) and output histories
+  L.plb = take(ne * sc.pl_maxb);
+  L.pla = take(ne * sc.pl_maxa);
+  L.mzb = take(nmz * (sc.dtc ? sc.mz_maxb : 0));
+  L.mza = take(nmz * (sc.dtc ? sc.mz_maxa : 0));
+  L.frb = take(nfr * (sc.dtc ? sc.fr_max : 0));
+  L.fra = take(nfr * (sc.dtc ? sc.fr_max : 0));
+  L.step = take(my * nu * sc.tlen > M * M ? my * nu * sc.tlen : M * M);  // prologue only
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -632,7 +643,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
 }
 
 
-template <int MAXM>
+template <int MAXM, bool DTC>
 __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
@@ -674,7 +685,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
-  const LdsLayout L = lds_layout(M, nx, nu, nin, ne, my, sc.tlen, sc.pl_maxb, sc.pl_maxa);
+  const LdsLayout L = lds_layout(sc, M);
   const int nxp = (nx + 1) & ~1;  // padded row length of A (x[nx] and the pad column are 0)
   double* sRi = lds + L.rinv;
   double* sA = lds + L.A;
@@ -694,6 +705,15 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   for (int e = lane; e < my * nu * sc.tlen; e += kWave) sstep[e] = sc.step[e];
   for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
   for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
+  if constexpr (DTC) {  // predictor model entries and filters (DTC_GPC_WW.m:40-46, mimofilter.m)
+    const int nmz = 2 * my * nu;
+    for (int e = lane; e < nmz * sc.mz_maxb; e += kWave) lds[L.mzb + e] = sc.mz_b[e];
+    for (int e = lane; e < nmz * sc.mz_maxa; e += kWave) lds[L.mza + e] = sc.mz_a[e];
+    for (int e = lane; e < my * sc.fr_max; e += kWave) {
+      lds[L.frb + e] = sc.fr_b[e];
+      lds[L.fra + e] = sc.fr_a[e];
+    }
+  }
   for (int e = lane; e < L.plb - L.x; e += kWave) lds[L.x + e] = 0.0;  // state + histories
   // per-lane constants in registers
   const int yoff_i = lane < my ? sc.yoff[lane] : 0;
@@ -1006,13 +1026,54 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     }
     lds_sync();
     PSTAMP(PROF_PLANT);
+    if constexpr (DTC) {
+      // predictor model entries on the controller's own input history (OptimalPredictor2.m:
+      // lsim(Pz, u) and lsim(Gz, u) kept as recursions): lanes e < my*nu are Pz, the next my*nu Gz
+      const int nmz = 2 * my * nu;
+      if (lane < nmz) {
+        const int j = lane % nu;
+        const double* mb = lds + L.mzb + lane * sc.mz_maxb;
+        const double* ma = lds + L.mza + lane * sc.mz_maxa;
+        double* mh = lds + L.mzh + lane * kYeHist;
+        const double* ur = sur + j * kURing;  // closed-loop input ring of MV j
+        const int mnb = sc.mz_nb[lane], mna = sc.mz_na[lane], moff = sc.mz_off[lane];
+        double a0 = 0.0, a1 = 0.0;
+        for (int l = moff; l < mnb; ++l) a0 += mb[l] * ur[(t - l) & (kURing - 1)];
+        for (int l = 1; l < mna; ++l) a1 -= ma[l] * mh[(t - l) & (kYeHist - 1)];
+        const double am = a0 + a1;
+        mh[t & (kYeHist - 1)] = am;
+        lds[L.smz + lane] = am;
+      }
+      lds_sync();
+    }
     if (lane < my) {
       const int i = lane;
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
+      // the measurement driving the free response: y, or the DTC predictor output
+      // yp = Gz*u + Fr*(y - Pz*u)  (OptimalPredictor2.m:24-40, DTC_GPC_WW.m:133-142)
+      double ym = y;
+      if constexpr (DTC) {
+        double ypz = 0.0, ygz = 0.0;
+        for (int j = 0; j < nu; ++j) {
+          ypz += lds[L.smz + i * nu + j];
+          ygz += lds[L.smz + my * nu + i * nu + j];
+        }
+        double* eh = lds + L.frh + i * 2 * kYeHist;  // eM history, then yfr history
+        double* fh = eh + kYeHist;
+        const double* fb = lds + L.frb + i * sc.fr_max;
+        const double* fa = lds + L.fra + i * sc.fr_max;
+        eh[t & (kYeHist - 1)] = y - ypz;
+        double yfr = 0.0;
+        const int nf = sc.fr_n[i];
+        for (int l = 0; l < nf; ++l) yfr += fb[l] * eh[(t - l) & (kYeHist - 1)];
+        for (int l = 1; l < nf; ++l) yfr -= fa[l] * fh[(t - l) & (kYeHist - 1)];
+        fh[t & (kYeHist - 1)] = yfr;
+        ym = ygz + yfr;
+      }
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
       if (regpath) {  // yd = [y(t-1), nabla y(t-1), ...] in registers
-        double cur = y, prev = yd[0];
+        double cur = ym, prev = yd[0];
 #pragma unroll
         for (int k = 1; k < kRegY; ++k) {
           if (k < nyh_i) {
@@ -1023,9 +1084,9 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
             sx[yoff_i + k] = nk;
           }
         }
-        yd[0] = y;
+        yd[0] = ym;
       } else {
-        double cur = y, prev = syprev[i];
+        double cur = ym, prev = syprev[i];
         for (int k = 1; k < nyh_i; ++k) {
           const double old = sx[yoff_i + k];
           const double nk = cur - prev;
@@ -1033,9 +1094,9 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
           cur = nk;
           prev = old;
         }
-        syprev[i] = y;
+        syprev[i] = ym;
       }
-      sx[yoff_i] = y - r_t;
+      sx[yoff_i] = ym - r_t;
       const double e1 = y - yr_t;
       j1 += e1 * e1;
       if (t >= sc.ink0) j22 += e1 * e1;
@@ -1118,7 +1179,7 @@ namespace mpct {
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {
   (void)N2;
   const int M = sc.nu * Nu;
-  LdsLayout L = lds_layout(M, sc.nx, sc.nu, sc.nin, sc.ne, sc.my, sc.tlen, sc.pl_maxb, sc.pl_maxa);
+  LdsLayout L = lds_layout(sc, M);
   return (long long)L.total * 8;
 }
 
@@ -1131,7 +1192,7 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
-  auto kern = gpc_closed_loop_kernel<MAXM>;
+  auto kern = sc.dtc ? gpc_closed_loop_kernel<MAXM, true> : gpc_closed_loop_kernel<MAXM, false>;
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {

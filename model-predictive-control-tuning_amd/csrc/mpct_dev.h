@@ -32,7 +32,7 @@ struct DevScenario {
   int nyh, nup;             // sizes of the two parts
   int wsq;                  // weights squared
   int ink0;                 // VNS inK, 0-based
-  int ne;                   // plant entries my*nin
+  int ne;                   // plant entries my*nin (nin = plant input columns incl. disturbances)
   int pl_maxb, pl_maxa;     // longest plant numerator (incl. delay) / denominator
   int regpath;              // every per-lane history / coefficient set fits the kReg* caps
   // tables (device pointers into one allocation)
@@ -50,6 +50,18 @@ struct DevScenario {
   const double* pl_a;   // [ne][pl_maxa]
   const double* bnd;    // [4][nu]  du_min, du_max, u_min, u_max
   const double* yref;   // [my][nit]
+  // DTC-GPC predictor (dtc = 1): model entries Pz (e < my*nu) and Gz (e >= my*nu), z^-1 form,
+  // and the robustness filters Fr_i, z^-1 form, delay 0
+  int dtc;
+  int mz_maxb, mz_maxa, fr_max;
+  const int* mz_nb;     // [2*my*nu]
+  const int* mz_na;
+  const int* mz_off;
+  const double* mz_b;   // [2*my*nu][mz_maxb]
+  const double* mz_a;   // [2*my*nu][mz_maxa]
+  const int* fr_n;      // [my]
+  const double* fr_b;   // [my][fr_max]
+  const double* fr_a;   // [my][fr_max]
 };
 
 struct DevOpts {

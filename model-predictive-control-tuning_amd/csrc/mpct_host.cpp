@@ -48,8 +48,15 @@ struct mpct_scenario {
   std::vector<double> phi;   // [my*n2max][nx]  reference layout (S | Hp)
   std::vector<double> phid;  // same rows on the device state basis (see create)
   int ne = 0, pl_maxb = 0, pl_maxa = 0;
+  int npin = 0;  // plant input columns: nu MVs, nd MDs, nq plant-only disturbances
   std::vector<int> pl_nb, pl_na, pl_off;
   std::vector<double> pl_b, pl_a;
+  // DTC-GPC predictor (abi >= 2): Pz and Gz entries (2*my*nu, z^-1 form) and the filters Fr_i
+  int dtc = 0, nq = 0;
+  int mz_maxb = 1, mz_maxa = 1, fr_max = 1;
+  std::vector<int> mz_nb, mz_na, mz_off;
+  std::vector<double> mz_b, mz_a, fr_b, fr_a;
+  std::vector<int> fr_n;
   std::vector<double> bnd;   // [4][nu]
   std::vector<double> yref;  // [my][nit]
   // device state
@@ -96,7 +103,10 @@ static void step_response(const mpct_dtf& d, int T, double* s) {
 extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenario** out) {
   if (!d || !out) return fail(MPCT_EINVAL, "null argument");
   *out = nullptr;
-  if (d->abi_version != MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
+  if (d->abi_version != 1 && d->abi_version != MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
+  const int dtc = d->abi_version >= 2 ? (d->dtc ? 1 : 0) : 0;
+  const int nq = d->abi_version >= 2 ? d->nq : 0;
+  if (nq < 0 || (nq > 0 && !d->dist)) return fail(MPCT_EINVAL, "nq > 0 needs dist");
   if (d->my < 1 || d->nu < 1 || d->nd < 0 || d->nit < 1 || d->n2_max < 1 || d->nu_max < 1)
     return fail(MPCT_EINVAL, "non-positive dimension");
   if (d->my > kMaxOut || d->nu + d->nd > kMaxIn) return fail(MPCT_ERANGE, "too many outputs/inputs");
@@ -111,6 +121,13 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   s->nu = d->nu;
   s->nd = d->nd;
   s->nin = d->nu + d->nd;
+  s->dtc = dtc;
+  s->nq = nq;
+  s->npin = s->nin + nq;
+  if (s->npin > kMaxIn) {
+    delete s;
+    return fail(MPCT_ERANGE, "too many plant inputs");
+  }
   s->nit = d->nit;
   s->n2max = d->n2_max;
   s->numax = d->nu_max;
@@ -198,7 +215,9 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       delete s;
       return fail(MPCT_EINVAL, "carima_A[i][0] must be 1");
     }
-    const int dd = s->n1[i] - 1;  // diophantine(A, N, d): N1 = d+1
+    // diophantine(A, N, d): N1 = d+1; DTC-GPC predicts from the delay-free yp (d = 0,
+    // DTC_GPC_WW.m:80) while MatG keeps the dmin+1 window
+    const int dd = s->dtc ? 0 : s->n1[i] - 1;
     std::vector<double> Ai(A, A + na + 1);
     std::vector<double> AD = conv(Ai, {1.0, -1.0});  // A~ = A*Delta (diophantine.m:35)
     const int nAD = (int)AD.size();                 // na + 2
@@ -263,12 +282,18 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       dst[0] = 1.0;
     }
   }
-  // ---- plant entries in z^-1 form (delay folded into b)
-  s->ne = my * nin;
+  // ---- plant entries in z^-1 form (delay folded into b); plant-only disturbance paths appended
+  // as columns nin..npin-1 of each output row
+  const int npin = s->npin;
+  s->ne = my * npin;
   s->pl_nb.resize(s->ne);
   s->pl_na.resize(s->ne);
+  auto plant_entry = [&](int e) -> const mpct_dtf& {
+    const int i = e / npin, j = e % npin;
+    return j < nin ? d->plant[i * nin + j] : d->dist[i * nq + (j - nin)];
+  };
   for (int e = 0; e < s->ne; ++e) {
-    const mpct_dtf& p = d->plant[e];
+    const mpct_dtf& p = plant_entry(e);
     if (p.len < 1 || !p.num || !p.den || p.den[0] == 0.0 || p.delay < 0) {
       delete s;
       return fail(MPCT_EINVAL, "bad plant entry");
@@ -277,7 +302,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     s->pl_na[e] = p.len;
     s->pl_maxb = std::max(s->pl_maxb, s->pl_nb[e]);
     s->pl_maxa = std::max(s->pl_maxa, s->pl_na[e]);
-    const int j = e % nin;
+    const int j = e % npin;
     if (j < nu && p.delay == 0 && p.num[0] != 0.0) {
       delete s;
       return fail(MPCT_EINVAL, "plant has direct feedthrough from an MV (algebraic loop)");
@@ -300,7 +325,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   s->pl_b.assign((size_t)s->ne * s->pl_maxb, 0.0);
   s->pl_a.assign((size_t)s->ne * s->pl_maxa, 0.0);
   for (int e = 0; e < s->ne; ++e) {
-    const mpct_dtf& p = d->plant[e];
+    const mpct_dtf& p = plant_entry(e);
     for (int k = 0; k < p.len; ++k) {
       s->pl_b[(size_t)e * s->pl_maxb + p.delay + k] = p.num[k] / p.den[0];
       s->pl_a[(size_t)e * s->pl_maxa + k] = p.den[k] / p.den[0];
@@ -311,6 +336,71 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     int o = 0;
     while (o < s->pl_nb[e] && s->pl_b[(size_t)e * s->pl_maxb + o] == 0.0) ++o;
     s->pl_off[e] = o;
+  }
+  if (s->dtc) {
+    // Pz entries (e < my*nu, real delays) and Gz entries (delays minus dmin_i = n1_i - 1,
+    // DTC_GPC_WW.m:40-46) in z^-1 form; filters Fr_i (mimofilter.m) with delay 0
+    const int nm = 2 * my * nu;
+    s->mz_nb.resize(nm);
+    s->mz_na.resize(nm);
+    s->mz_off.resize(nm);
+    for (int e = 0; e < nm; ++e) {
+      const int k = e % (my * nu), i = k / nu, j = k % nu;
+      const mpct_dtf& m = d->model[i * nin + j];
+      const int del = e < my * nu ? m.delay : m.delay - (s->n1[i] - 1);
+      if (del < 0) {
+        delete s;
+        return fail(MPCT_EINVAL, "DTC: model delay below dmin (n1 - 1)");
+      }
+      s->mz_nb[e] = del + m.len;
+      s->mz_na[e] = m.len;
+      s->mz_maxb = std::max(s->mz_maxb, s->mz_nb[e]);
+      s->mz_maxa = std::max(s->mz_maxa, s->mz_na[e]);
+    }
+    if (s->mz_maxb > kMaxTaps || s->mz_maxa > kYeHist) {
+      delete s;
+      return fail(MPCT_ERANGE, "DTC: model entry too long for the device history rings");
+    }
+    s->mz_b.assign((size_t)nm * s->mz_maxb, 0.0);
+    s->mz_a.assign((size_t)nm * s->mz_maxa, 0.0);
+    for (int e = 0; e < nm; ++e) {
+      const int k = e % (my * nu), i = k / nu, j = k % nu;
+      const mpct_dtf& m = d->model[i * nin + j];
+      const int del = e < my * nu ? m.delay : m.delay - (s->n1[i] - 1);
+      for (int q2 = 0; q2 < m.len; ++q2) {
+        s->mz_b[(size_t)e * s->mz_maxb + del + q2] = m.num[q2] / m.den[0];
+        s->mz_a[(size_t)e * s->mz_maxa + q2] = m.den[q2] / m.den[0];
+      }
+      int o2 = 0;
+      while (o2 < s->mz_nb[e] && s->mz_b[(size_t)e * s->mz_maxb + o2] == 0.0) ++o2;
+      s->mz_off[e] = o2;
+    }
+    s->fr_n.assign(my, 1);
+    for (int i = 0; i < my; ++i)
+      if (d->filter) s->fr_n[i] = d->filter[i].len;
+    for (int i = 0; i < my; ++i) s->fr_max = std::max(s->fr_max, s->fr_n[i]);
+    if (s->fr_max > kYeHist) {
+      delete s;
+      return fail(MPCT_ERANGE, "DTC: filter order too high (len <= 8)");
+    }
+    s->fr_b.assign((size_t)my * s->fr_max, 0.0);
+    s->fr_a.assign((size_t)my * s->fr_max, 0.0);
+    for (int i = 0; i < my; ++i) {
+      if (!d->filter) {
+        s->fr_b[(size_t)i * s->fr_max] = 1.0;
+        s->fr_a[(size_t)i * s->fr_max] = 1.0;
+        continue;
+      }
+      const mpct_dtf& f = d->filter[i];
+      if (f.len < 1 || !f.num || !f.den || f.den[0] == 0.0 || f.delay != 0) {
+        delete s;
+        return fail(MPCT_EINVAL, "DTC: bad filter entry (delay must be 0)");
+      }
+      for (int q2 = 0; q2 < f.len; ++q2) {
+        s->fr_b[(size_t)i * s->fr_max + q2] = f.num[q2] / f.den[0];
+        s->fr_a[(size_t)i * s->fr_max + q2] = f.den[q2] / f.den[0];
+      }
+    }
   }
   s->bnd.resize(4 * nu);
   for (int n = 0; n < nu; ++n) {
@@ -405,6 +495,14 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   size_t o_pla = put(s->pl_a.data(), s->pl_a.size() * 8);
   size_t o_bnd = put(s->bnd.data(), s->bnd.size() * 8);
   size_t o_yref = put(s->yref.data(), s->yref.size() * 8);
+  size_t o_mznb = put(s->mz_nb.data(), s->mz_nb.size() * 4);
+  size_t o_mzna = put(s->mz_na.data(), s->mz_na.size() * 4);
+  size_t o_mzoff = put(s->mz_off.data(), s->mz_off.size() * 4);
+  size_t o_mzb = put(s->mz_b.data(), s->mz_b.size() * 8);
+  size_t o_mza = put(s->mz_a.data(), s->mz_a.size() * 8);
+  size_t o_frn = put(s->fr_n.data(), s->fr_n.size() * 4);
+  size_t o_frb = put(s->fr_b.data(), s->fr_b.size() * 8);
+  size_t o_fra = put(s->fr_a.data(), s->fr_a.size() * 8);
   void* dp = nullptr;
   if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
   if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -415,8 +513,8 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   DevScenario& ds = s->ds;
   ds.my = s->my;
   ds.nu = s->nu;
-  ds.nd = s->nd;
-  ds.nin = s->nin;
+  ds.nd = s->nd + s->nq;  // ring-fed plant inputs (their signals are v's rows)
+  ds.nin = s->npin;       // plant input columns
   ds.nit = s->nit;
   ds.n2max = s->n2max;
   ds.numax = s->numax;
@@ -450,6 +548,18 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.pl_a = reinterpret_cast<const double*>(b + o_pla);
   ds.bnd = reinterpret_cast<const double*>(b + o_bnd);
   ds.yref = reinterpret_cast<const double*>(b + o_yref);
+  ds.dtc = s->dtc;
+  ds.mz_maxb = s->mz_maxb;
+  ds.mz_maxa = s->mz_maxa;
+  ds.fr_max = s->fr_max;
+  ds.mz_nb = reinterpret_cast<const int*>(b + o_mznb);
+  ds.mz_na = reinterpret_cast<const int*>(b + o_mzna);
+  ds.mz_off = reinterpret_cast<const int*>(b + o_mzoff);
+  ds.mz_b = reinterpret_cast<const double*>(b + o_mzb);
+  ds.mz_a = reinterpret_cast<const double*>(b + o_mza);
+  ds.fr_n = reinterpret_cast<const int*>(b + o_frn);
+  ds.fr_b = reinterpret_cast<const double*>(b + o_frb);
+  ds.fr_a = reinterpret_cast<const double*>(b + o_fra);
   s->dtab = dp;
   s->dev = dev;
   return MPCT_OK;
@@ -470,7 +580,7 @@ static int check_args(mpct_scenario* s, int64_t C, int32_t nref, const int32_t* 
   if (C < 0 || nref < 1) return fail(MPCT_EINVAL, "C < 0 or nref < 1");
   if (C * (int64_t)nref > 0x7fffffffLL) return fail(MPCT_ERANGE, "too many simulations in one call");
   if (C > 0 && (!N2 || !Nu || !delta || !lambda || !r)) return fail(MPCT_EINVAL, "null input pointer");
-  if (s->nd > 0 && !v) return fail(MPCT_EINVAL, "v required when nd > 0");
+  if (s->nd + s->nq > 0 && !v) return fail(MPCT_EINVAL, "v required when nd + nq > 0");
   return MPCT_OK;
 }
 
@@ -483,6 +593,7 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   if (!out) return fail(MPCT_EINVAL, "null result");
   rc = ensure_device(s, opts ? opts->device : -1);
   if (rc) return rc;
+  if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
   if (C == 0) return MPCT_OK;
   DevOpts dop = make_opts(opts);
   DevResult dr{out->J1, out->j21, out->j22, out->Jnu, out->status, out->qp_iters,
@@ -541,7 +652,7 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
     return o;
   };
   size_t o_N2 = slot(C * 4), o_Nu = slot(C * 4), o_d = slot(C * my * 8), o_l = slot(C * nu * 8);
-  size_t o_r = slot((size_t)nref * my * nit * 8), o_v = slot((size_t)nref * nd * nit * 8);
+  size_t o_r = slot((size_t)nref * my * nit * 8), o_v = slot((size_t)nref * (nd + s->nq) * nit * 8);
   size_t o_J1 = slot(S * my * 8), o_j21 = slot(S * my * 8), o_j22 = slot(S * my * 8), o_Jnu = slot(S * nu * 8);
   size_t o_st = slot(S * 4), o_it = slot(S * 8);
   size_t o_y = traj ? slot(S * my * nit * 8) : 0, o_u = traj ? slot(S * nu * nit * 8) : 0;
@@ -559,7 +670,7 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
   };
   if (!h2d(o_N2, N2, C * 4) || !h2d(o_Nu, Nu, C * 4) || !h2d(o_d, delta, C * my * 8) ||
       !h2d(o_l, lambda, C * nu * 8) || !h2d(o_r, r, (size_t)nref * my * nit * 8) ||
-      (nd > 0 && !h2d(o_v, v, (size_t)nref * nd * nit * 8)))
+      (nd + s->nq > 0 && !h2d(o_v, v, (size_t)nref * (nd + s->nq) * nit * 8)))
     return fail(MPCT_EDEVICE, "hipMemcpy(inputs) failed");
   mpct_result dres{};
   dres.J1 = reinterpret_cast<double*>(b + o_J1);
@@ -581,7 +692,7 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
                               reinterpret_cast<const double*>(b + o_d),
                               reinterpret_cast<const double*>(b + o_l), nref,
                               reinterpret_cast<const double*>(b + o_r),
-                              nd > 0 ? reinterpret_cast<const double*>(b + o_v) : nullptr, opts, &dres,
+                              nd + s->nq > 0 ? reinterpret_cast<const double*>(b + o_v) : nullptr, opts, &dres,
                               nullptr);
   if (rc) return rc;
   if (hipDeviceSynchronize() != hipSuccess) return fail(MPCT_EDEVICE, "kernel execution failed");
@@ -604,11 +715,15 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   DevScenario ds{};
   ds.my = s->my;
   ds.nu = s->nu;
-  ds.nin = s->nin;
+  ds.nin = s->npin;
   ds.nx = s->nx;
   ds.ne = s->ne;
   ds.tlen = s->tlen;
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
+  ds.dtc = s->dtc;
+  ds.mz_maxb = s->mz_maxb;
+  ds.mz_maxa = s->mz_maxa;
+  ds.fr_max = s->fr_max;
   return lds_bytes_for(ds, N2, Nu);
 }

@@ -40,6 +40,10 @@ class MpctScenarioDesc(C.Structure):
         ("du_min", c_double_p), ("du_max", c_double_p),
         ("u_min", c_double_p), ("u_max", c_double_p),
         ("yref", c_double_p),
+        ("dtc", C.c_int32),
+        ("filter", C.POINTER(MpctDtf)),
+        ("nq", C.c_int32),
+        ("dist", C.POINTER(MpctDtf)),
     ]
 
 
@@ -59,7 +63,7 @@ EXPORTS = [
     "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
 ]
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 ST_QP_MAXITER, ST_QP_INFEAS, ST_NONFINITE, ST_SKIPPED, ST_BADHORIZON = 1, 2, 4, 8, 16
 
 _lib = None

@@ -38,7 +38,8 @@ class Scenario:
     ``exact_carima``: exact LCM (toolbox-equivalent) vs BA_MIMO's rounded roots."""
 
     def __init__(self, plant, model, nu, du_min, du_max, u_min, u_max, yref, n2_max, nu_max,
-                 Ts=1.0, window="toolbox", weights_squared=True, exact_carima=True, vns_ink=10):
+                 Ts=1.0, window="toolbox", weights_squared=True, exact_carima=True, vns_ink=10,
+                 dtc=False, filters=None, dist=None):
         self.lib = _lib.load()
         self.plant, self.model = plant, model
         self.my, self.nin = len(model), len(model[0])
@@ -53,6 +54,12 @@ class Scenario:
         self.dp, self.na, self.nb = dp, na, nb
         self.dmin = dp[:, : self.nu].min(axis=1)
         n1 = np.ones(self.my, dtype=np.int32) if window == "toolbox" else (self.dmin + 1).astype(np.int32)
+        # DTC-GPC (DTC_GPC_WW.m): GPC window, deltaUFree on the delays net of dmin (dnz)
+        self.dtc = bool(dtc)
+        self.nq = len(dist[0]) if dist else 0
+        if self.dtc and window != "gpc":
+            raise ValueError("DTC mode uses the GPC window (MatG/diophantine N1 = dmin+1)")
+        dp_desc = (dp - self.dmin[:, None]) if self.dtc else dp
         keep = []  # keep every buffer alive for the descriptor's lifetime
 
         def dtf_array(P):
@@ -72,7 +79,7 @@ class Scenario:
             [np.asarray(B[i][j], dtype=float) / A[i][0] for i in range(self.my) for j in range(self.nin)]))
         na32 = np.ascontiguousarray(na, dtype=np.int32)
         nb32 = np.ascontiguousarray(nb.ravel(), dtype=np.int32)
-        dp32 = np.ascontiguousarray(dp.ravel(), dtype=np.int32)
+        dp32 = np.ascontiguousarray(dp_desc.ravel(), dtype=np.int32)
         bnds = [np.ascontiguousarray(np.broadcast_to(np.asarray(b, dtype=float), (self.nu,)))
                 for b in (du_min, du_max, u_min, u_max)]
         self.bounds = bnds
@@ -89,6 +96,28 @@ class Scenario:
         d.na, d.carima_A, d.nb, d.carima_B, d.dp = _ip(na32), _dp(A_cat), _ip(nb32), _dp(B_cat), _ip(dp32)
         d.du_min, d.du_max, d.u_min, d.u_max = (_dp(b) for b in bnds)
         d.yref = _dp(self.yref)
+        d.dtc = int(self.dtc)
+        d.nq = self.nq
+        if filters is not None:
+            farr = (_lib.MpctDtf * self.my)()
+            for i, t in enumerate(filters):
+                num = np.ascontiguousarray(t.num, dtype=float)
+                den = np.ascontiguousarray(t.den, dtype=float)
+                keep.extend([num, den])
+                farr[i] = _lib.MpctDtf(len(num), _dp(num), _dp(den), int(t.delay))
+            keep.append(farr)
+            d.filter = farr
+        if self.nq:
+            darr = (_lib.MpctDtf * (self.my * self.nq))()
+            for i in range(self.my):
+                for j in range(self.nq):
+                    t = dist[i][j]
+                    num = np.ascontiguousarray(t.num, dtype=float)
+                    den = np.ascontiguousarray(t.den, dtype=float)
+                    keep.extend([num, den])
+                    darr[i * self.nq + j] = _lib.MpctDtf(len(num), _dp(num), _dp(den), int(t.delay))
+            keep.append(darr)
+            d.dist = darr
         h = C.c_void_p()
         rc = self.lib.mpct_scenario_create(C.byref(d), C.byref(h))
         if rc != 0:
@@ -160,8 +189,9 @@ def eval_batch(sc: Scenario, N2, Nu, delta, lam, refs, v=None, open_loop=False, 
     nref = refs.shape[0]
     S = Cn * nref
     vv = None
-    if sc.nd:
-        vv = np.ascontiguousarray(np.asarray(v, dtype=float).reshape(nref, sc.nd, sc.nit))
+    if sc.nd + sc.nq:
+        vv = np.ascontiguousarray(np.broadcast_to(np.asarray(v, dtype=float).reshape(-1, sc.nd + sc.nq, sc.nit),
+                                                  (nref, sc.nd + sc.nq, sc.nit)))
     res = EvalResult(J1=np.zeros((S, sc.my)), j21=np.zeros((S, sc.my)), j22=np.zeros((S, sc.my)),
                      Jnu=np.zeros((S, sc.nu)), status=np.zeros(S, dtype=np.int32),
                      qp_iters=np.zeros(S, dtype=np.int64), nref=nref)

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .matlab import DTF, conv, mround, poly, roots, step_dtf
+from .matlab import DTF, conv, lsim_dtf, mround, poly, roots, step_dtf
 
 
 # ---------------------------------------------------------------------------------------------
@@ -231,3 +231,179 @@ def blkdiag(*mats):
         r += a.shape[0]
         c += a.shape[1]
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# DTC-GPC robustness filter and predictor (config 1)
+# ---------------------------------------------------------------------------------------------
+def _mldivide(A, B):
+    """MATLAB A\\B: square -> LU solve; rectangular underdetermined -> the basic solution of a
+    column-pivoted QR (at most rank(A) nonzeros), as mldivide returns it."""
+    import scipy.linalg as sla
+
+    A = np.asarray(A, dtype=float)
+    B = np.asarray(B, dtype=float)
+    if A.shape[0] == A.shape[1]:
+        return np.linalg.solve(A, B)
+    Q, R, piv = sla.qr(A, mode="economic", pivoting=True)
+    r = int(np.sum(np.abs(np.diag(R)) > max(A.shape) * np.finfo(float).eps * abs(R[0, 0])))
+    x = np.zeros(A.shape[1])
+    x[piv[:r]] = sla.solve_triangular(R[:r, :r], (Q.T @ B)[:r])
+    return x
+
+
+def filtro_siso(num, den, d: int, alfa: float, raio: float, kn: int = 2):
+    """filtro_siso.m:12-96.  Robustness filter Fr(z) = Nr(z)/Dr(z) for the fast model
+    num/den (z, descending powers) with dead time d: the unwanted poles |p| >= raio are
+    cancelled (Sylvester system A X = B, :52-83) and Dr = (z - alfa)^nk (:42-45).  kn is unused
+    by the reference.  Returns (Nr, Dr); (1, 1) when no pole is unwanted (:89-93)."""
+    polos = roots(den)
+    p_ind = [p for p in polos if abs(p) >= raio]            # :27
+    nm = len(p_ind)
+    nk = nm
+    pd = 0
+    if d == 0:                                               # :31-35
+        pd = 2
+        nk += pd
+    px = np.real(poly([1.0] + list(p_ind)))                  # :37-39
+    Dr = np.array([1.0])
+    for _ in range(nk):
+        Dr = conv(Dr, [1.0, -alfa])
+    ordem = (len(Dr) - 1) + d                                # :46
+    lpx = len(px)
+    A = np.zeros((ordem + 1, ordem + 1 + pd))
+    ip = 1
+    for j in range(ordem + 2 - d, ordem + 2 + pd):           # :52-65 (1-based columns)
+        pn = 1
+        for i in range(ip, ordem + 2):
+            if pn <= lpx:
+                A[i - 1, j - 1] = px[pn - 1]
+                pn += 1
+        ip += 1
+    j = 1
+    for i in range(d + 1, ordem + 2):                        # :67-70
+        A[i - 1, j - 1] = 1.0
+        j += 1
+    B = np.zeros(ordem + 1)
+    B[0] = 1.0
+    B[1:len(Dr)] = Dr[1:]
+    X = _mldivide(A, B)
+    Nr = X[:ordem + 1 - d]
+    if nm == 0:
+        return np.array([1.0]), np.array([1.0])
+    return np.asarray(Nr, dtype=float), Dr
+
+
+def mimofilter(Pd, alfa: float = 0.7, raio: float = 0.8, kn: int = 2):
+    """mimofilter.m:16-50: one filter per output on the product of the row's nonzero entries
+    (H(i) = prod_j G(i,j), delay dmin(i)).  Pd: my x n DTF.  Returns a list of (Nr, Dr)."""
+    my = len(Pd)
+    Fr = []
+    for i in range(my):
+        dmin_i = min(Pd[i][j].iodelay for j in range(len(Pd[i])))
+        num, den = np.array([1.0]), np.array([1.0])
+        for j in range(len(Pd[i])):
+            if np.sum(Pd[i][j].num) != 0:
+                num = conv(num, np.trim_zeros(Pd[i][j].num, "f"))
+                den = conv(den, Pd[i][j].den)
+        if np.sum(num) == 0:
+            Fr.append((np.array([1.0]), np.array([1.0])))
+        else:
+            Fr.append(filtro_siso(num, den, int(dmin_i), alfa, raio, kn))
+    return Fr
+
+
+def optimal_predictor2(Fr, Pz, Gz, u, y, k: int):
+    """OptimalPredictor2.m:24-40, full history (the reference structure, O(k) per call):
+    yp = Gz*u + Fr*(y - Pz*u) over samples 1..k."""
+    from .matlab import lsim_mimo
+
+    U = np.asarray(u)[:, :k]
+    ypz = lsim_mimo(Pz, U)
+    ygz = lsim_mimo(Gz, U)
+    eM = np.asarray(y)[:, :k] - ypz
+    yfr = np.zeros_like(eM)
+    for i, (Nr, Dr) in enumerate(Fr):
+        yfr[i] = lsim_dtf(DTF(Nr, Dr, 0), eM[i])
+    return ygz + yfr
+
+
+def woodberry_models(deltak: float = 0.0, deltaL: float = 0.0, Ts: float = 1.0):
+    """DTC_GPC_WW.m:18-41 models, CondMin-free variant L = R = I (CondMin's fmincon result is
+    not unique and no WoodBerry tuning file is committed): real plant P (gain / delay
+    mismatch deltak, deltaL), nominal Pn, disturbance path Pq -- all discretised ZOH (lsim of
+    the continuous plant with 'zoh' input is exactly this)."""
+    from .matlab import c2d_zoh
+
+    K = np.array([[12.8, -18.9], [6.6, -19.4]])
+    tau = np.array([[16.7, 21.0], [10.9, 14.4]])
+    L = np.array([[1.0, 2.0], [2.0, 1.0]])
+    P = [[c2d_zoh([K[i, j] * (1 + deltak)], [tau[i, j], 1.0], Ts, L[i, j] + deltaL) for j in range(2)]
+         for i in range(2)]
+    Pn = [[c2d_zoh([K[i, j]], [tau[i, j], 1.0], Ts, L[i, j]) for j in range(2)] for i in range(2)]
+    Pq = [[c2d_zoh([3.8], [14.9, 1.0], Ts, 8.1)], [c2d_zoh([4.9], [13.2, 1.0], Ts, 3.4)]]
+    return P, Pn, Pq
+
+
+def dtc_gpc_ww(p=(3, 3), m=(3, 3), lam=(1.0, 1.0), delta=(1.0, 1.0), nit: int = 200, deltak: float = 0.0,
+               deltaL: float = 0.0, alfa: float = 0.7, raio: float = 0.8, disturbance: bool = True,
+               filt: bool = True):
+    """DTC_GPC_WW.m:59-164 (config 1), reference structure: every step re-simulates the whole
+    history with lsim (plant, disturbance path and the three predictor models), O(nit^2).
+    L = R = I.  Returns dict(y, u, yp, r, q)."""
+    P, Pn, Pq = woodberry_models(deltak, deltaL)
+    my = ny = 2
+    Pnz = Pn
+    Bp, Ap, dp = descomp_mpc(Pnz)
+    dmin = np.array([dp[i, :].min() for i in range(my)])
+    Gnz = [[DTF(Pnz[i][j].num, Pnz[i][j].den, Pnz[i][j].iodelay - dmin[i]) for j in range(ny)]
+           for i in range(my)]
+    dnz = dp - dmin[:, None]
+    p = list(p)
+    m = list(m)
+    W = np.diag(np.concatenate([lam[i] * np.ones(m[i]) for i in range(ny)]))   # :67-71
+    Q = np.diag(np.concatenate([delta[i] * np.ones(p[i]) for i in range(my)]))  # :72-76
+    B, A, na, nb = ba_mimo(Bp, Ap)                           # :79
+    E, En, F = diophantine_mimo(A, p, [0, 0])                # :80
+    S = blkdiag(*[F[i][: p[i], :] for i in range(my)])
+    H, _ = mat_g(Pnz, p, m, dp)                              # :89
+    uG = delta_u_free(B, En, p, dnz)                         # :91
+    Hp = cell2mat2(uG)
+    duM = (nb + dnz).max(axis=0)                             # :93
+    up = np.zeros(int(duM.sum()))
+    S1 = H.T @ Q @ H + W
+    S1 = (S1 + S1.T) / 2
+    K = np.linalg.solve(S1, H.T @ Q)                         # :98-100
+    Km = np.stack([K[int(sum(m[:i]))] for i in range(ny)])
+    Fr = mimofilter(Pnz, alfa, raio) if filt else [(np.array([1.0]), np.array([1.0]))] * my
+    r = np.zeros((my, nit))
+    r[0, 10:] = 0.8                                          # :117-119 (1-based 11, 61)
+    r[1, 60:] = 0.5
+    q = np.zeros((1, nit))
+    if disturbance:
+        q[0, 140:] = -0.25                                   # :123-124
+    u = np.zeros((ny, nit))
+    ue = np.zeros((ny, nit))
+    y = np.zeros((my, nit))
+    yp = np.zeros((my, nit))
+    from .matlab import lsim_mimo
+
+    for k in range(4, nit + 1):                              # :126 (1-based k)
+        yq = lsim_mimo(Pq, q[:, :k])
+        yk = lsim_mimo(P, u[:, :k]) + yq
+        y[:, :k] = yk
+        ye = yk
+        ypk = optimal_predictor2(Fr, Pnz, Gnz, ue, ye, k)
+        yp[:, :k] = ypk
+        Yd = np.concatenate([ypk[j, k - 1 - np.arange(na[j] + 1)] for j in range(my)])
+        Ref = np.concatenate([np.full(p[i], r[i, k - 1]) for i in range(my)])
+        yf = Hp @ up + S @ Yd
+        dU = Km @ (Ref - yf)
+        off = 0
+        for i in range(ny):
+            blk = up[off: off + duM[i]].copy()
+            up[off: off + duM[i]] = np.concatenate([[dU[i]], blk[:-1]])
+            off += duM[i]
+        ue[:, k - 1] = (ue[:, k - 2] if k > 1 else 0.0) + dU
+        u[:, k - 1] = ue[:, k - 1]
+    return dict(y=y, u=u, yp=yp, r=r, q=q, Fr=Fr, Km=Km, S=S, Hp=Hp, dmin=dmin, duM=duM)

@@ -35,7 +35,19 @@ def test_header_and_exports_agree(built):
 def test_abi_version(built):
     from mpct import _lib
 
-    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 1
+    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 2
+
+
+def test_abi_v1_descriptor_accepted(built, monkeypatch):
+    """Version-1 descriptors (no DTC / disturbance fields) are still accepted; the v2 fields are
+    ignored for them."""
+    from mpct import _lib
+    from mpct.scenarios import shell3x3
+
+    _lib.load()
+    monkeypatch.setattr(_lib, "ABI_VERSION", 1)
+    sc, r, yref = shell3x3(n2_max=10, nu_max=2)
+    assert sc.dims()["nx"] == 35
 
 
 @pytest.fixture(scope="module")
@@ -155,8 +167,8 @@ def _kernel_meta(text):
     out = {}
     for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, flags=re.S):
         body = m.group(2)
-        maxm = int(re.search(r"kernelILi(\d+)E", m.group(1)).group(1))
-        out[maxm] = dict(
+        mm = re.search(r"kernelILi(\d+)ELb(\d)E", m.group(1))
+        out[(int(mm.group(1)), int(mm.group(2)))] = dict(
             scratch=int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", body).group(1)),
             vgpr=int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", body).group(1)))
     return out
@@ -172,5 +184,5 @@ def test_kernel_isa_invariants(built):
     assert "s_swappc_b64" not in text
     assert "flat_load" not in text and "flat_store" not in text
     meta = _kernel_meta(text)
-    assert set(meta) == {16, 32, 64}
-    assert meta[16]["scratch"] == 0 and meta[16]["vgpr"] <= 256, meta[16]
+    assert set(meta) == {(m, d) for m in (16, 32, 64) for d in (0, 1)}   # (MAXM, DTC)
+    assert meta[(16, 0)]["scratch"] == 0 and meta[(16, 0)]["vgpr"] <= 256, meta[(16, 0)]
