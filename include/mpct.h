@@ -108,6 +108,12 @@ typedef struct mpct_scenario_desc {
   const mpct_dtf* filter;
   int32_t nq;
   const mpct_dtf* dist;
+  /* nplant     number of simulated-plant variants (plant-mismatch Monte-Carlo draws, SURVEY
+   *            §8d config 4); 0 or 1 -> the single plant above.  Simulation s = c*nref + k runs
+   *            variant k % nplant (the draws ride on the reference dimension)
+   * plant_var  [nplant][my*(nu+nd)] variant plants (replace plant when nplant > 1)           */
+  int32_t nplant;
+  const mpct_dtf* plant_var;
 } mpct_scenario_desc;
 
 typedef struct mpct_scenario mpct_scenario;

@@ -703,8 +703,11 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
 
   // ------------------------------------------------------------------ prologue
   for (int e = lane; e < my * nu * sc.tlen; e += kWave) sstep[e] = sc.step[e];
-  for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
-  for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
+  // this simulation's plant variant (Monte-Carlo draw k % nvar)
+  const int pvar = sc.nvar > 1 ? kref % sc.nvar : 0;
+  const int pve = pvar * ne;
+  for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[(long long)pve * sc.pl_maxb + e];
+  for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[(long long)pve * sc.pl_maxa + e];
   if constexpr (DTC) {  // predictor model entries and filters (DTC_GPC_WW.m:40-46, mimofilter.m)
     const int nmz = 2 * my * nu;
     for (int e = lane; e < nmz * sc.mz_maxb; e += kWave) lds[L.mzb + e] = sc.mz_b[e];
@@ -730,9 +733,9 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   const int ecopy = lane / ne;
   const int ee = lane - ecopy * ne;
   const int ej = ee % nin;
-  const int e_nb = (lane < ne * 2) ? sc.pl_nb[ee] : 0;
-  const int e_na = (lane < ne * 2) ? sc.pl_na[ee] : 0;
-  const int e_off = (lane < ne * 2) ? sc.pl_off[ee] : 0;
+  const int e_nb = (lane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
+  const int e_na = (lane < ne * 2) ? sc.pl_na[pve + ee] : 0;
+  const int e_off = (lane < ne * 2) ? sc.pl_off[pve + ee] : 0;
   const double* dl = deltav + c * my;
   const double* lm = lambdav + c * nu;
   lds_sync();

@@ -53,6 +53,7 @@ struct DevScenario {
   // DTC-GPC predictor (dtc = 1): model entries Pz (e < my*nu) and Gz (e >= my*nu), z^-1 form,
   // and the robustness filters Fr_i, z^-1 form, delay 0
   int dtc;
+  int nvar;               // plant variants: pl_* tables are [nvar][ne]; simulation k uses k % nvar
   int mz_maxb, mz_maxa, fr_max;
   const int* mz_nb;     // [2*my*nu]
   const int* mz_na;

@@ -49,6 +49,7 @@ struct mpct_scenario {
   std::vector<double> phid;  // same rows on the device state basis (see create)
   int ne = 0, pl_maxb = 0, pl_maxa = 0;
   int npin = 0;  // plant input columns: nu MVs, nd MDs, nq plant-only disturbances
+  int nvar = 1;  // plant variants (Monte-Carlo draws); tables are [nvar][ne]
   std::vector<int> pl_nb, pl_na, pl_off;
   std::vector<double> pl_b, pl_a;
   // DTC-GPC predictor (abi >= 2): Pz and Gz entries (2*my*nu, z^-1 form) and the filters Fr_i
@@ -106,6 +107,8 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   if (d->abi_version != 1 && d->abi_version != MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
   const int dtc = d->abi_version >= 2 ? (d->dtc ? 1 : 0) : 0;
   const int nq = d->abi_version >= 2 ? d->nq : 0;
+  const int nplant = (d->abi_version >= 2 && d->nplant > 1) ? d->nplant : 1;
+  if (nplant > 1 && !d->plant_var) return fail(MPCT_EINVAL, "nplant > 1 needs plant_var");
   if (nq < 0 || (nq > 0 && !d->dist)) return fail(MPCT_EINVAL, "nq > 0 needs dist");
   if (d->my < 1 || d->nu < 1 || d->nd < 0 || d->nit < 1 || d->n2_max < 1 || d->nu_max < 1)
     return fail(MPCT_EINVAL, "non-positive dimension");
@@ -124,6 +127,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   s->dtc = dtc;
   s->nq = nq;
   s->npin = s->nin + nq;
+  s->nvar = nplant;
   if (s->npin > kMaxIn) {
     delete s;
     return fail(MPCT_ERANGE, "too many plant inputs");
@@ -286,13 +290,16 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   // as columns nin..npin-1 of each output row
   const int npin = s->npin;
   s->ne = my * npin;
-  s->pl_nb.resize(s->ne);
-  s->pl_na.resize(s->ne);
-  auto plant_entry = [&](int e) -> const mpct_dtf& {
+  const int nve = s->nvar * s->ne;  // entries over all variants: ev = variant*ne + e
+  s->pl_nb.resize(nve);
+  s->pl_na.resize(nve);
+  auto plant_entry = [&](int ev) -> const mpct_dtf& {
+    const int v = ev / s->ne, e = ev % s->ne;
     const int i = e / npin, j = e % npin;
-    return j < nin ? d->plant[i * nin + j] : d->dist[i * nq + (j - nin)];
+    if (j >= nin) return d->dist[i * nq + (j - nin)];
+    return s->nvar > 1 ? d->plant_var[(size_t)v * my * nin + i * nin + j] : d->plant[i * nin + j];
   };
-  for (int e = 0; e < s->ne; ++e) {
+  for (int e = 0; e < nve; ++e) {
     const mpct_dtf& p = plant_entry(e);
     if (p.len < 1 || !p.num || !p.den || p.den[0] == 0.0 || p.delay < 0) {
       delete s;
@@ -302,7 +309,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     s->pl_na[e] = p.len;
     s->pl_maxb = std::max(s->pl_maxb, s->pl_nb[e]);
     s->pl_maxa = std::max(s->pl_maxa, s->pl_na[e]);
-    const int j = e % npin;
+    const int j = (e % s->ne) % npin;
     if (j < nu && p.delay == 0 && p.num[0] != 0.0) {
       delete s;
       return fail(MPCT_EINVAL, "plant has direct feedthrough from an MV (algebraic loop)");
@@ -322,17 +329,17 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
     delete s;
     return fail(MPCT_ERANGE, "plant entry too long for the device history rings");
   }
-  s->pl_b.assign((size_t)s->ne * s->pl_maxb, 0.0);
-  s->pl_a.assign((size_t)s->ne * s->pl_maxa, 0.0);
-  for (int e = 0; e < s->ne; ++e) {
+  s->pl_b.assign((size_t)nve * s->pl_maxb, 0.0);
+  s->pl_a.assign((size_t)nve * s->pl_maxa, 0.0);
+  for (int e = 0; e < nve; ++e) {
     const mpct_dtf& p = plant_entry(e);
     for (int k = 0; k < p.len; ++k) {
       s->pl_b[(size_t)e * s->pl_maxb + p.delay + k] = p.num[k] / p.den[0];
       s->pl_a[(size_t)e * s->pl_maxa + k] = p.den[k] / p.den[0];
     }
   }
-  s->pl_off.assign(s->ne, 0);
-  for (int e = 0; e < s->ne; ++e) {
+  s->pl_off.assign(nve, 0);
+  for (int e = 0; e < nve; ++e) {
     int o = 0;
     while (o < s->pl_nb[e] && s->pl_b[(size_t)e * s->pl_maxb + o] == 0.0) ++o;
     s->pl_off[e] = o;
@@ -529,7 +536,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.pl_maxa = s->pl_maxa;
   {
     bool rp = s->pl_maxa - 1 <= kRegA;
-    for (int e = 0; e < s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
+    for (int e = 0; e < s->nvar * s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
     for (int n = 0; n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
     for (int i = 0; i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
     ds.regpath = rp ? 1 : 0;
@@ -549,6 +556,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.bnd = reinterpret_cast<const double*>(b + o_bnd);
   ds.yref = reinterpret_cast<const double*>(b + o_yref);
   ds.dtc = s->dtc;
+  ds.nvar = s->nvar;
   ds.mz_maxb = s->mz_maxb;
   ds.mz_maxa = s->mz_maxa;
   ds.fr_max = s->fr_max;

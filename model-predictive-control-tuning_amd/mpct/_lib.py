@@ -44,6 +44,8 @@ class MpctScenarioDesc(C.Structure):
         ("filter", C.POINTER(MpctDtf)),
         ("nq", C.c_int32),
         ("dist", C.POINTER(MpctDtf)),
+        ("nplant", C.c_int32),
+        ("plant_var", C.POINTER(MpctDtf)),
     ]
 
 

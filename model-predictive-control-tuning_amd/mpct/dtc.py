@@ -102,3 +102,48 @@ def woodberry_dtc(n2_max: int = 30, nu_max: int = 10, nit: int = 200, deltak: fl
                   n2_max=n2_max, nu_max=nu_max, Ts=Ts, window="gpc", weights_squared=False,
                   exact_carima=False, dtc=True, filters=filters, dist=Pq)
     return sc, r, q
+
+
+# --------------------------------------------------------------------------------------------
+def woodberry_mc_plants(draws: int, seed: int = 20250307, gain_spread: float = 0.2, max_dshift: int = 2,
+                        Ts: float = 1.0):
+    """SURVEY §8d config 4 plant-mismatch draws modelled on DTC_GPC_WW.m:18-19 (deltak, deltaL):
+    each entry's gain x (1 + U(-gain_spread, gain_spread)) and delay + U{0..max_dshift} * Ts,
+    numpy default_rng(seed).  Returns a list of 2x2 plants (mpct.lti.Tf)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(draws):
+        g = 1.0 + rng.uniform(-gain_spread, gain_spread, (2, 2))
+        dl = rng.integers(0, max_dshift + 1, (2, 2))
+        out.append([[c2d([WB_K[i, j] * g[i, j]], [WB_TAU[i, j], 1.0], Ts, WB_L[i, j] + dl[i, j] * Ts)
+                     for j in range(2)] for i in range(2)])
+    return out
+
+
+def woodberry_mc(draws: int = 32, n2_max: int = 30, nu_max: int = 10, nit: int = 200, seed: int = 20250307,
+                 alfa: float = 0.7, raio: float = 0.8):
+    """Config 4 scenario: the DTC-GPC of woodberry_dtc evaluated over `draws` mismatched plants
+    (variant k runs with reference row k).  Returns (Scenario, refs [draws, 2, nit],
+    v [draws, 1, nit], plants)."""
+    from .engine import Scenario
+
+    base, r, q = woodberry_dtc(n2_max=2, nu_max=1, nit=nit)        # for r, q and the model
+    plants = woodberry_mc_plants(draws, seed)
+    Pn = base.model
+    Pq = [[c2d([WB_QK[i]], [WB_QTAU[i], 1.0], 1.0, WB_QL[i])] for i in range(2)]
+    inf = np.full(2, np.inf)
+    sc = Scenario(plants[0], Pn, nu=2, du_min=-inf, du_max=inf, u_min=-inf, u_max=inf, yref=r,
+                  n2_max=n2_max, nu_max=nu_max, Ts=1.0, window="gpc", weights_squared=False,
+                  exact_carima=False, dtc=True, filters=mimofilter(Pn, alfa, raio), dist=Pq,
+                  plant_variants=plants)
+    base.close()
+    refs = np.broadcast_to(r, (draws, 2, nit)).copy()
+    v = np.broadcast_to(q, (draws, 1, nit)).copy()
+    return sc, refs, v, plants
+
+
+def robust_scores(J1, C: int, draws: int):
+    """Per-candidate robustness scores over the draws: (mean, worst) of sum_i J1_i, where J1 is
+    the engine's (C*draws, my) cost array in simulation order (candidate-major)."""
+    J = np.asarray(J1).reshape(C, draws, -1).sum(axis=2)
+    return J.mean(axis=1), J.max(axis=1)

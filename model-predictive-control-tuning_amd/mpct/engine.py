@@ -39,7 +39,7 @@ class Scenario:
 
     def __init__(self, plant, model, nu, du_min, du_max, u_min, u_max, yref, n2_max, nu_max,
                  Ts=1.0, window="toolbox", weights_squared=True, exact_carima=True, vns_ink=10,
-                 dtc=False, filters=None, dist=None):
+                 dtc=False, filters=None, dist=None, plant_variants=None):
         self.lib = _lib.load()
         self.plant, self.model = plant, model
         self.my, self.nin = len(model), len(model[0])
@@ -118,6 +118,21 @@ class Scenario:
                     darr[i * self.nq + j] = _lib.MpctDtf(len(num), _dp(num), _dp(den), int(t.delay))
             keep.append(darr)
             d.dist = darr
+        self.nplant = len(plant_variants) if plant_variants else 1
+        if plant_variants and len(plant_variants) > 1:
+            n = self.my * self.nin
+            varr = (_lib.MpctDtf * (len(plant_variants) * n))()
+            for v, Pv in enumerate(plant_variants):
+                for i in range(self.my):
+                    for j in range(self.nin):
+                        t = Pv[i][j]
+                        num = np.ascontiguousarray(t.num, dtype=float)
+                        den = np.ascontiguousarray(t.den, dtype=float)
+                        keep.extend([num, den])
+                        varr[v * n + i * self.nin + j] = _lib.MpctDtf(len(num), _dp(num), _dp(den), int(t.delay))
+            keep.append(varr)
+            d.nplant = len(plant_variants)
+            d.plant_var = varr
         h = C.c_void_p()
         rc = self.lib.mpct_scenario_create(C.byref(d), C.byref(h))
         if rc != 0:

@@ -81,3 +81,46 @@ def test_dtc_batch_of_candidates(gpu):
     np.testing.assert_array_equal(one.J1[0], res.J1[5])
     ref = dtc_gpc_ww()
     np.testing.assert_allclose(res.J1[0], np.sum((ref["y"] - ref["r"]) ** 2, axis=1), rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_dtc_monte_carlo_variants(gpu):
+    """Config 4: simulation (c, k) runs plant variant k -- bitwise equal to a single-plant
+    scenario built with that draw, and a uniform-mismatch draw equals the oracle loop."""
+    from mpct.dtc import robust_scores, woodberry_dtc, woodberry_mc
+    from mpct.engine import Scenario, eval_batch
+    from oracle.dtcgpc import dtc_gpc_ww
+
+    D, C = 4, 6
+    sc, refs, v, plants = woodberry_mc(draws=D, n2_max=10, nu_max=5)
+    rng = np.random.default_rng(5)
+    N2 = rng.integers(3, 11, C).astype(np.int32)
+    Nu = np.minimum(rng.integers(1, 6, C), N2).astype(np.int32)
+    d = 10.0 ** rng.uniform(-1, 1, (C, 2))
+    l = 10.0 ** rng.uniform(-1, 1, (C, 2))
+    res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
+    assert np.all(res.status == 0)
+    for k in (0, 2, 3):
+        one_sc, r, q = woodberry_dtc(n2_max=10, nu_max=5)
+        # the same disturbance paths as the MC scenario, one plant
+        from mpct.dtc import WB_QK, WB_QL, WB_QTAU, mimofilter
+        from mpct.lti import c2d
+        Pq = [[c2d([WB_QK[i]], [WB_QTAU[i], 1.0], 1.0, WB_QL[i])] for i in range(2)]
+        single = Scenario(plants[k], one_sc.model, nu=2, du_min=-np.full(2, np.inf), du_max=np.full(2, np.inf),
+                          u_min=-np.full(2, np.inf), u_max=np.full(2, np.inf), yref=r, n2_max=10, nu_max=5,
+                          window="gpc", weights_squared=False, exact_carima=False, dtc=True,
+                          filters=mimofilter(one_sc.model), dist=Pq)
+        rs = eval_batch(single, N2, Nu, d, l, r[None], v=q[None])
+        np.testing.assert_array_equal(rs.J1, res.J1.reshape(C, D, 2)[:, k])
+    mean, worst = robust_scores(res.J1, C, D)
+    assert np.all(worst >= mean)
+    # a uniform gain/delay mismatch draw against the reference-structured loop
+    from mpct.dtc import WB_K, WB_L, WB_TAU
+    from mpct.lti import c2d as c2d_
+    Pu = [[c2d_([WB_K[i, j] * 1.1], [WB_TAU[i, j], 1.0], 1.0, WB_L[i, j] + 1.0) for j in range(2)] for i in range(2)]
+    sc2, r2, q2 = woodberry_dtc(n2_max=10, nu_max=5, deltak=0.1, deltaL=1.0)
+    ru = eval_batch(sc2, np.array([3], np.int32), np.array([3], np.int32), np.ones((1, 2)), np.ones((1, 2)),
+                    r2[None], v=q2[None], want_traj=True)
+    ref = dtc_gpc_ww(deltak=0.1, deltaL=1.0)
+    assert _trel(ru.y[0], ref["y"]) < TRAJ_RTOL
+    assert all(Pu[i][j].delay == sc2.plant[i][j].delay for i in range(2) for j in range(2))
