@@ -1,0 +1,199 @@
+// gi_core.h — Goldfarb-Idnani dual active-set machinery in J-form, shared by the closed-loop
+// kernels.  Lanes 0..M-1 are the QP rows (M = QP dimension <= MAXM <= 64).  The constraint
+// bookkeeping (which ids are active) is the caller's: gi_add / gi_drop call mark(S, id, on).
+#pragma once
+#include "wave_ops.h"
+
+namespace mpct {
+
+// Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
+// family) in its factored, numerically stable form.  H = R'R;  J (M x M) with
+// H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].
+// For the most violated constraint p:  d = J'n_p,  z = J(:,q:) d(q:) (primal direction),
+// r = R_A^-1 d(0:q) (dual direction), beta = n_p'z = |d(q:)|^2.  Adding p applies ONE
+// Householder reflector to J(:,q:) mapping d(q:) onto alpha e_q (its dot products are
+// z - alpha J(:,q), so the add costs one sqrt) and appends [d(0:q); alpha] to R_A; dropping
+// constraint k re-triangularises R_A with Givens rotations applied to J's columns.
+//
+// Warm start across the receding-horizon steps: the constraint normals do not depend on the
+// step (only the bounds do), so the factorisation of the previous step's final active set is
+// kept (J and R_A in LDS, multipliers and ids in lanes).  Each QP first solves the equality-constrained problem on
+// that set from the unconstrained minimiser x_u (x = x_u + J_A w, R_A'w = b_A - N_A'x_u,
+// lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
+// and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
+// convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
+// R^-1 (re-adding the set) after 4M rotations, which bounds the orthogonality drift of the
+// rotated J (unbounded drift measured 3.5e-5 relative on the metric grid; with the rebuild
+// 7.5e-10).
+template <int MAXM>
+struct GIState {
+  double rdg;       // 1 / R_A(lane, lane)
+  double uw;        // multiplier of active constraint `lane`
+  int ww;           // id (4*m + kind) of active constraint `lane`
+  unsigned act;     // active bits of this lane's 4 constraints (row m = lane)
+  int q;            // active-set size (wave-uniform)
+  int nrot;         // rotations applied to J since it was last built from R^-1 (uniform)
+  bool jinit;       // J holds a factorisation consistent with the active set (uniform)
+};
+
+template <int MAXM>
+__device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
+  S.rdg = 0.0;
+  S.uw = 0.0;
+  S.ww = -1;
+  S.act = 0;
+  S.q = 0;
+  S.nrot = 0;
+  S.jinit = false;
+}
+
+template <int MAXM>
+__device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
+                                             bool row) {
+  const int lane = threadIdx.x;
+  if (row)
+    for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
+  S.nrot = 0;
+  S.jinit = true;
+  lds_sync();
+}
+
+// d = J'n_p = sg * (sum of J's rows j0..mp): lane k sums column k of J (contiguous in JT); d -> sd
+template <int MAXM>
+__device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, int j0, int mp, double sg,
+                                          bool row) {
+  const int lane = threadIdx.x;
+  double dk = 0.0;
+  if (row) {
+    for (int j = j0; j <= mp; ++j) dk += sJT[lane * M + j];
+    dk *= sg;
+    sd[lane] = dk;
+  }
+  return dk;
+}
+
+// z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
+__device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row) {
+  const int lane = threadIdx.x;
+  double z0 = 0.0, z1 = 0.0;
+  if (row) {
+    int k = q;
+    for (; k + 1 < M; k += 2) {
+      z0 += sJT[k * M + lane] * sd[k];
+      z1 += sJT[(k + 1) * M + lane] * sd[k + 1];
+    }
+    if (k < M) z0 += sJT[k * M + lane] * sd[k];
+  }
+  return z0 + z1;
+}
+
+// r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
+template <int MAXM>
+__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
+  const int lane = threadIdx.x;
+  double ck = lane < S.q ? c : 0.0, rk = 0.0;
+  for (int w = S.q - 1; w >= 0; --w) {
+    const double rw = bcast(ck * S.rdg, w);
+    if (lane == w) rk = rw;
+    if (lane < w) ck -= sRA[lane * M + w] * rw;
+  }
+  return rk;
+}
+
+// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
+template <int MAXM, class Mark>
+__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
+                                       int p, double dk, double beta, double zm, double upm, bool row,
+                                       const Mark& mark) {
+  const int lane = threadIdx.x;
+  const int q = S.q;
+  const double dq = bcast(dk, q);
+  const double nrm = sqrt(beta);
+  const double alpha = dq > 0.0 ? -nrm : nrm;
+  const double vq = dq - alpha;
+  const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
+  if (row) {
+    const double jq = sJT[q * M + lane];
+    const double f = (zm - alpha * jq) * two_vtv;
+    sJT[q * M + lane] = jq - f * vq;
+    for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
+  }
+  if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  if (lane == q) {
+    sRA[q * M + q] = alpha;
+    S.rdg = 1.0 / alpha;
+    S.uw = upm;
+    S.ww = p;
+  }
+  mark(S, p, true);
+  S.q = q + 1;
+  S.nrot += 1;
+  lds_sync();
+}
+
+// remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
+template <int MAXM, class Mark>
+__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
+                                        const Mark& mark) {
+  const int lane = threadIdx.x;
+  const int q = S.q;
+  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
+  mark(S, idk, false);
+  if (lane < q) {  // remove column kd (lanes = rows)
+    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
+  }
+  {
+    const double un = lane_next<MAXM>(S.uw);
+    const int wn = lane_next_i<MAXM>(S.ww);
+    if (lane >= kd && lane < q - 1) {
+      S.uw = un;
+      S.ww = wn;
+    }
+  }
+  lds_sync();
+  // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
+  for (int jj = kd; jj < q - 1; ++jj) {
+    {
+      const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
+      const double rho = sqrt(a * a + b * b);
+      if (rho != 0.0) {
+        const double ri = 1.0 / rho;
+        const double cs = a * ri, sn = b * ri;
+        if (lane >= jj && lane < q - 1) {
+          const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
+          sRA[jj * M + lane] = cs * r0 + sn * r1;
+          sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
+        }
+        if (lane < M) {
+          const double j0v = sJT[jj * M + lane], j1v = sJT[(jj + 1) * M + lane];
+          sJT[jj * M + lane] = cs * j0v + sn * j1v;
+          sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
+        }
+        S.nrot += 1;
+      }
+      lds_sync();
+    }
+  }
+  const int qn = q - 1;
+  if (lane == qn) {
+    S.uw = 0.0;
+    S.ww = -1;
+  }
+  if (lane < qn) S.rdg = 1.0 / sRA[lane * M + lane];
+  S.q = qn;
+  lds_sync();
+}
+
+
+// active-flag bookkeeping of the box constraints p = 4m + kind: bit kind of lane m
+struct BoxMark {
+  template <class St>
+  __device__ __forceinline__ void operator()(St& S, int p, bool on) const {
+    if ((int)threadIdx.x == (p >> 2)) {
+      if (on) S.act |= 1u << (p & 3);
+      else S.act &= ~(1u << (p & 3));
+    }
+  }
+};
+
+}  // namespace mpct

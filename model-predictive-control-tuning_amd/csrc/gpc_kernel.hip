@@ -22,6 +22,7 @@
 #include <math.h>
 
 #include "mpct_dev.h"
+#include "gi_core.h"
 
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 1
@@ -69,107 +70,6 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   return L;
 }
 
-// ------------------------------------------------------------------------------------------
-// wave helpers
-__device__ __forceinline__ void lds_sync() {
-  // one-wave workgroup: LDS requests of a wave complete in order; wait for this lane's and order
-  // the compiler's memory operations around the hand-off
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ double bcast(double v, int src) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
-  return __hiloint2double(hi, lo);
-}
-
-template <int CTRL>
-__device__ __forceinline__ double dppd(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-// DPP controls: quad_perm(1,0,3,2), quad_perm(2,3,0,1), row_half_mirror, row_mirror
-constexpr int kQx1 = 0xB1, kQx2 = 0x4E, kHalfMirror = 0x141, kMirror = 0x140;
-
-// sum over lanes 0..15 (every lane of row 0 gets it; callers zero inactive lanes)
-__device__ __forceinline__ double row_sum(double v) {
-  v += dppd<kQx1>(v);
-  v += dppd<kQx2>(v);
-  v += dppd<kHalfMirror>(v);
-  v += dppd<kMirror>(v);
-  return v;
-}
-__device__ __forceinline__ void row_argmin_step(double& v, int& id, double pv, int pi) {
-  if (pv < v || (pv == v && pi < id)) {
-    v = pv;
-    id = pi;
-  }
-}
-__device__ __forceinline__ void row_argmin(double& v, int& id) {
-  row_argmin_step(v, id, dppd<kQx1>(v), dppi<kQx1>(id));
-  row_argmin_step(v, id, dppd<kQx2>(v), dppi<kQx2>(id));
-  row_argmin_step(v, id, dppd<kHalfMirror>(v), dppi<kHalfMirror>(id));
-  row_argmin_step(v, id, dppd<kMirror>(v), dppi<kMirror>(id));
-}
-
-__device__ __forceinline__ double wave_sum64(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-__device__ __forceinline__ void wave_argmin64(double& v, int& id) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double ov = __shfl_xor(v, off, 64);
-    int oid = __shfl_xor(id, off, 64);
-    if (ov < v || (ov == v && oid < id)) {
-      v = ov;
-      id = oid;
-    }
-  }
-}
-
-// sum over the four 16-lane rows (lanes l, l+16, l+32, l+48), result in every row:
-// v_permlane16_swap then v_permlane32_swap (gfx950), no LDS round trip
-__device__ __forceinline__ double row4_sum(double v) {
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const double a = __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
-  lo = __double2loint(a);
-  hi = __double2hiint(a);
-  auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
-}
-
-// reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
-template <int MAXM>
-__device__ __forceinline__ double qsum(double v) {
-  if constexpr (MAXM <= 16) {
-    return bcast(row_sum(v), 0);
-  } else {
-    return wave_sum64(v);
-  }
-}
-template <int MAXM>
-__device__ __forceinline__ void qargmin(double& v, int& id) {
-  if constexpr (MAXM <= 16) {
-    row_argmin(v, id);
-    v = bcast(v, 0);
-    id = __builtin_amdgcn_readlane(id, 0);
-  } else {
-    wave_argmin64(v, id);
-  }
-}
-
 // constraint p = 4*m + kind on move m = n*Nu + l:
 //   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
 //   kind 2:  sum_{l'<=l} du_(n,l') >= u_min - u_prev    kind 3: -sum >= -(u_max - u_prev)
@@ -209,239 +109,6 @@ __device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m
     s[2] = pre - (rc.umin - up);
     s[3] = (rc.umax - up) - pre;
   }
-}
-
-#ifdef MPCT_PROFILE
-#define PSTAMP(k)                                              \
-  do {                                                         \
-    __builtin_amdgcn_sched_barrier(0);                         \
-    unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
-    pacc[k] += now_ - pprev;                                   \
-    pprev = now_;                                              \
-    __builtin_amdgcn_sched_barrier(0);                         \
-  } while (0)
-#else
-#define PSTAMP(k) \
-  do {            \
-  } while (0)
-#endif
-
-// ------------------------------------------------------------------------------------------
-// lane shifts by one within the QP rows: DPP row_shl/row_shr when the rows fit one DPP row
-template <int MAXM>
-__device__ __forceinline__ double lane_next(double v) {  // lane i receives lane i+1
-  if constexpr (MAXM <= 16) return dppd<0x101>(v);
-  else return __shfl_down(v, 1, 64);
-}
-template <int MAXM>
-__device__ __forceinline__ double lane_prev(double v) {  // lane i receives lane i-1
-  if constexpr (MAXM <= 16) return dppd<0x111>(v);
-  else return __shfl_up(v, 1, 64);
-}
-template <int MAXM>
-__device__ __forceinline__ int lane_next_i(int v) {
-  if constexpr (MAXM <= 16) return dppi<0x101>(v);
-  else return __shfl_down(v, 1, 64);
-}
-
-// inclusive prefix sum of x over the lanes of one MV block (lane position l within its block):
-// the amplitude rows of the QP.  DPP row_shr Hillis-Steele scan when the rows fit one DPP row.
-template <int MAXM>
-__device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row, double* sxc) {
-  if constexpr (MAXM <= 16) {
-    double pre = x, t;
-    if (Nu > 1) { t = dppd<0x111>(pre); if (l >= 1) pre += t; }
-    if (Nu > 2) { t = dppd<0x112>(pre); if (l >= 2) pre += t; }
-    if (Nu > 4) { t = dppd<0x114>(pre); if (l >= 4) pre += t; }
-    if (Nu > 8) { t = dppd<0x118>(pre); if (l >= 8) pre += t; }
-    return pre;
-  } else {
-    const int lane = threadIdx.x;  // sxc holds the M QP rows only
-    if (row) sxc[lane] = x;
-    lds_sync();
-    double pre = 0.0;
-    if (row)
-      for (int j = lane - l; j <= lane; ++j) pre += sxc[j];
-    lds_sync();
-    return pre;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
-// family) in its factored, numerically stable form.  H = R'R;  J (M x M) with
-// H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].
-// For the most violated constraint p:  d = J'n_p,  z = J(:,q:) d(q:) (primal direction),
-// r = R_A^-1 d(0:q) (dual direction), beta = n_p'z = |d(q:)|^2.  Adding p applies ONE
-// Householder reflector to J(:,q:) mapping d(q:) onto alpha e_q (its dot products are
-// z - alpha J(:,q), so the add costs one sqrt) and appends [d(0:q); alpha] to R_A; dropping
-// constraint k re-triangularises R_A with Givens rotations applied to J's columns.
-//
-// Warm start across the receding-horizon steps: the constraint normals do not depend on the
-// step (only the bounds do), so the factorisation of the previous step's final active set is
-// kept (J in registers, R_A in LDS).  Each QP first solves the equality-constrained problem on
-// that set from the unconstrained minimiser x_u (x = x_u + J_A w, R_A'w = b_A - N_A'x_u,
-// lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
-// and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
-// convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
-// R^-1 (re-adding the set) after 4M rotations, which bounds the orthogonality drift of the
-// rotated J (unbounded drift measured 3.5e-5 relative on the metric grid; with the rebuild
-// 7.5e-10).
-template <int MAXM>
-struct GIState {
-  double rdg;       // 1 / R_A(lane, lane)
-  double uw;        // multiplier of active constraint `lane`
-  int ww;           // id (4*m + kind) of active constraint `lane`
-  unsigned act;     // active bits of this lane's 4 constraints (row m = lane)
-  int q;            // active-set size (wave-uniform)
-  int nrot;         // rotations applied to J since it was last built from R^-1 (uniform)
-  bool jinit;       // J holds a factorisation consistent with the active set (uniform)
-};
-
-template <int MAXM>
-__device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
-  S.rdg = 0.0;
-  S.uw = 0.0;
-  S.ww = -1;
-  S.act = 0;
-  S.q = 0;
-  S.nrot = 0;
-  S.jinit = false;
-}
-
-template <int MAXM>
-__device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
-                                             bool row) {
-  const int lane = threadIdx.x;
-  if (row)
-    for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
-  S.nrot = 0;
-  S.jinit = true;
-  lds_sync();
-}
-
-// d = J'n_p = sg * (sum of J's rows j0..mp): lane k sums column k of J (contiguous in JT); d -> sd
-template <int MAXM>
-__device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, int j0, int mp, double sg,
-                                          bool row) {
-  const int lane = threadIdx.x;
-  double dk = 0.0;
-  if (row) {
-    for (int j = j0; j <= mp; ++j) dk += sJT[lane * M + j];
-    dk *= sg;
-    sd[lane] = dk;
-  }
-  return dk;
-}
-
-// z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
-__device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row) {
-  const int lane = threadIdx.x;
-  double z0 = 0.0, z1 = 0.0;
-  if (row) {
-    int k = q;
-    for (; k + 1 < M; k += 2) {
-      z0 += sJT[k * M + lane] * sd[k];
-      z1 += sJT[(k + 1) * M + lane] * sd[k + 1];
-    }
-    if (k < M) z0 += sJT[k * M + lane] * sd[k];
-  }
-  return z0 + z1;
-}
-
-// r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
-template <int MAXM>
-__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
-  const int lane = threadIdx.x;
-  double ck = lane < S.q ? c : 0.0, rk = 0.0;
-  for (int w = S.q - 1; w >= 0; --w) {
-    const double rw = bcast(ck * S.rdg, w);
-    if (lane == w) rk = rw;
-    if (lane < w) ck -= sRA[lane * M + w] * rw;
-  }
-  return rk;
-}
-
-// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
-template <int MAXM>
-__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
-                                       int p, double dk, double beta, double zm, double upm, bool row) {
-  const int lane = threadIdx.x;
-  const int q = S.q;
-  const double dq = bcast(dk, q);
-  const double nrm = sqrt(beta);
-  const double alpha = dq > 0.0 ? -nrm : nrm;
-  const double vq = dq - alpha;
-  const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
-  if (row) {
-    const double jq = sJT[q * M + lane];
-    const double f = (zm - alpha * jq) * two_vtv;
-    sJT[q * M + lane] = jq - f * vq;
-    for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
-  }
-  if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
-  if (lane == q) {
-    sRA[q * M + q] = alpha;
-    S.rdg = 1.0 / alpha;
-    S.uw = upm;
-    S.ww = p;
-  }
-  if (lane == (p >> 2)) S.act |= 1u << (p & 3);
-  S.q = q + 1;
-  S.nrot += 1;
-  lds_sync();
-}
-
-// remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
-template <int MAXM>
-__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd) {
-  const int lane = threadIdx.x;
-  const int q = S.q;
-  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
-  if (lane == (idk >> 2)) S.act &= ~(1u << (idk & 3));
-  if (lane < q) {  // remove column kd (lanes = rows)
-    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
-  }
-  {
-    const double un = lane_next<MAXM>(S.uw);
-    const int wn = lane_next_i<MAXM>(S.ww);
-    if (lane >= kd && lane < q - 1) {
-      S.uw = un;
-      S.ww = wn;
-    }
-  }
-  lds_sync();
-  // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
-  for (int jj = kd; jj < q - 1; ++jj) {
-    {
-      const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
-      const double rho = sqrt(a * a + b * b);
-      if (rho != 0.0) {
-        const double ri = 1.0 / rho;
-        const double cs = a * ri, sn = b * ri;
-        if (lane >= jj && lane < q - 1) {
-          const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
-          sRA[jj * M + lane] = cs * r0 + sn * r1;
-          sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
-        }
-        if (lane < M) {
-          const double j0v = sJT[jj * M + lane], j1v = sJT[(jj + 1) * M + lane];
-          sJT[jj * M + lane] = cs * j0v + sn * j1v;
-          sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
-        }
-        S.nrot += 1;
-      }
-      lds_sync();
-    }
-  }
-  const int qn = q - 1;
-  if (lane == qn) {
-    S.uw = 0.0;
-    S.ww = -1;
-  }
-  if (lane < qn) S.rdg = 1.0 / sRA[lane * M + lane];
-  S.q = qn;
-  lds_sync();
 }
 
 // normal of constraint p = 4m + kind: rows j0..m of the MV block, sign
@@ -519,7 +186,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
           lds_sync();
           const double zm = gi_z(sJT, sd, v, M, row);
           const double uk = S.uw;
-          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row);
+          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row, BoxMark{});
           if (lane == v) S.uw = uk;
           ++it;
         }
@@ -549,7 +216,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(S, sJT, sRA, M, kd);
+        gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{});
         ++it;
       }
       if (!row) xm = 0.0;
@@ -624,11 +291,11 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
       upm += t;
       sp += t * beta;
       if (full) {
-        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row);
+        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
         PSTAMP(PROF_QADD);
         break;
       }
-      gi_drop<MAXM>(S, sJT, sRA, M, kdrop);
+      gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{});
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;

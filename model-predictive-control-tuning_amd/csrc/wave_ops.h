@@ -1,0 +1,171 @@
+// wave_ops.h — one-wavefront building blocks shared by the closed-loop kernels (gpc_kernel.hip,
+// mdband_kernel.hip): LDS hand-off fence, readlane broadcast, DPP / permlane reductions over the
+// QP-row lanes, lane shifts and the per-MV-block prefix sum.  Every helper is force-inlined: the
+// kernels rely on lds_sync() (lgkmcnt only), which is only correct when no helper is outlined
+// into a FLAT-addressed call (checked on the ISA by __graft_entry__.kernel_isa()).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "mpct_dev.h"
+
+namespace mpct {
+
+// ------------------------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ void lds_sync() {
+  // one-wave workgroup: LDS requests of a wave complete in order; wait for this lane's and order
+  // the compiler's memory operations around the hand-off
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double bcast(double v, int src) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// DPP controls: quad_perm(1,0,3,2), quad_perm(2,3,0,1), row_half_mirror, row_mirror
+constexpr int kQx1 = 0xB1, kQx2 = 0x4E, kHalfMirror = 0x141, kMirror = 0x140;
+
+// sum over lanes 0..15 (every lane of row 0 gets it; callers zero inactive lanes)
+__device__ __forceinline__ double row_sum(double v) {
+  v += dppd<kQx1>(v);
+  v += dppd<kQx2>(v);
+  v += dppd<kHalfMirror>(v);
+  v += dppd<kMirror>(v);
+  return v;
+}
+__device__ __forceinline__ void row_argmin_step(double& v, int& id, double pv, int pi) {
+  if (pv < v || (pv == v && pi < id)) {
+    v = pv;
+    id = pi;
+  }
+}
+__device__ __forceinline__ void row_argmin(double& v, int& id) {
+  row_argmin_step(v, id, dppd<kQx1>(v), dppi<kQx1>(id));
+  row_argmin_step(v, id, dppd<kQx2>(v), dppi<kQx2>(id));
+  row_argmin_step(v, id, dppd<kHalfMirror>(v), dppi<kHalfMirror>(id));
+  row_argmin_step(v, id, dppd<kMirror>(v), dppi<kMirror>(id));
+}
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ void wave_argmin64(double& v, int& id) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double ov = __shfl_xor(v, off, 64);
+    int oid = __shfl_xor(id, off, 64);
+    if (ov < v || (ov == v && oid < id)) {
+      v = ov;
+      id = oid;
+    }
+  }
+}
+
+// sum over the four 16-lane rows (lanes l, l+16, l+32, l+48), result in every row:
+// v_permlane16_swap then v_permlane32_swap (gfx950), no LDS round trip
+__device__ __forceinline__ double row4_sum(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
+  lo = __double2loint(a);
+  hi = __double2hiint(a);
+  auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
+}
+
+// reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
+template <int MAXM>
+__device__ __forceinline__ double qsum(double v) {
+  if constexpr (MAXM <= 16) {
+    return bcast(row_sum(v), 0);
+  } else {
+    return wave_sum64(v);
+  }
+}
+template <int MAXM>
+__device__ __forceinline__ void qargmin(double& v, int& id) {
+  if constexpr (MAXM <= 16) {
+    row_argmin(v, id);
+    v = bcast(v, 0);
+    id = __builtin_amdgcn_readlane(id, 0);
+  } else {
+    wave_argmin64(v, id);
+  }
+}
+
+#ifdef MPCT_PROFILE
+#define PSTAMP(k)                                              \
+  do {                                                         \
+    __builtin_amdgcn_sched_barrier(0);                         \
+    unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
+    pacc[k] += now_ - pprev;                                   \
+    pprev = now_;                                              \
+    __builtin_amdgcn_sched_barrier(0);                         \
+  } while (0)
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+// ------------------------------------------------------------------------------------------
+// lane shifts by one within the QP rows: DPP row_shl/row_shr when the rows fit one DPP row
+template <int MAXM>
+__device__ __forceinline__ double lane_next(double v) {  // lane i receives lane i+1
+  if constexpr (MAXM <= 16) return dppd<0x101>(v);
+  else return __shfl_down(v, 1, 64);
+}
+template <int MAXM>
+__device__ __forceinline__ double lane_prev(double v) {  // lane i receives lane i-1
+  if constexpr (MAXM <= 16) return dppd<0x111>(v);
+  else return __shfl_up(v, 1, 64);
+}
+template <int MAXM>
+__device__ __forceinline__ int lane_next_i(int v) {
+  if constexpr (MAXM <= 16) return dppi<0x101>(v);
+  else return __shfl_down(v, 1, 64);
+}
+
+// inclusive prefix sum of x over the lanes of one MV block (lane position l within its block):
+// the amplitude rows of the QP.  DPP row_shr Hillis-Steele scan when the rows fit one DPP row.
+template <int MAXM>
+__device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row, double* sxc) {
+  if constexpr (MAXM <= 16) {
+    double pre = x, t;
+    if (Nu > 1) { t = dppd<0x111>(pre); if (l >= 1) pre += t; }
+    if (Nu > 2) { t = dppd<0x112>(pre); if (l >= 2) pre += t; }
+    if (Nu > 4) { t = dppd<0x114>(pre); if (l >= 4) pre += t; }
+    if (Nu > 8) { t = dppd<0x118>(pre); if (l >= 8) pre += t; }
+    return pre;
+  } else {
+    const int lane = threadIdx.x;  // sxc holds the M QP rows only
+    if (row) sxc[lane] = x;
+    lds_sync();
+    double pre = 0.0;
+    if (row)
+      for (int j = lane - l; j <= lane; ++j) pre += sxc[j];
+    lds_sync();
+    return pre;
+  }
+}
+
+}  // namespace mpct

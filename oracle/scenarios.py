@@ -107,3 +107,66 @@ def candidate_grid(C=4096, my=3, nu=3, N2=30, Nu=5, seed=20250307, fx=None):
     N2v = np.full(C, N2, dtype=np.int32)
     Nuv = np.full(C, Nu, dtype=np.int32)
     return N2v, Nuv, delta, lam
+
+
+# ---------------------------------------------------------------------------------------------
+# Shell 7x5 (config 3): MPC-Tuning/Shell7x5.m, nominal = true (e1..e5 = 0, :38-43)
+SHELL7_K = np.array([[4.05, 1.77, 5.88, 1.20, 1.44], [5.39, 5.72, 6.9, 1.52, 1.83],
+                     [3.66, 1.65, 5.53, 1.16, 1.27], [5.92, 2.54, 8.10, 1.73, 1.79],
+                     [4.13, 2.38, 6.23, 1.31, 1.26], [4.06, 4.18, 6.53, 1.19, 1.17],
+                     [4.38, 4.42, 7.2, 1.14, 1.26]])          # Shell7x5.m:73-91 [Gs Ds]
+SHELL7_TAU = np.array([[50, 60, 50, 45, 40], [50, 60, 40, 25, 20], [9, 30, 40, 11, 6],
+                       [12, 27, 20, 5, 19], [8, 19, 10, 2, 22], [13, 33, 9, 19, 24],
+                       [33, 44, 19, 24, 32]], dtype=float)
+SHELL7_L = np.array([[27, 28, 27, 27, 27], [18, 14, 15, 15, 15], [2, 20, 2, 0, 0], [11, 12, 2, 0, 0],
+                     [5, 7, 2, 0, 0], [8, 4, 1, 0, 0], [20, 22, 0, 0, 0]], dtype=float)
+SHELL7_TS = 4.0
+SHELL7_NIT = 200
+SHELL7_YMX = np.array([0.005, 0.005, 0.5, 0.5, 0.5, 0.5, 0.5])   # Shell7x5.m:106-107
+SHELL7_ECR = np.array([0.1, 0.5, 1, 1, 1, 1, 1])                   # Shell7x5.m:143-152
+
+
+def shell7x5_plant_scaled(L, R):
+    """Pze = L * c2d([Gs Ds], Ts, 'zoh') * R  (Shell7x5.m:93-98, MPCTuning.m:162)."""
+    return [[c2d_zoh([SHELL7_K[i, j]], [SHELL7_TAU[i, j], 1.0], SHELL7_TS, SHELL7_L[i, j]).scaled(L[i] * R[j])
+             for j in range(5)] for i in range(7)]
+
+
+def shell7x5_yref(nit=SHELL7_NIT, tmd=20):
+    """Shell7x5.m:128-135: Xref(i, tmd:tmd+5) = Ymx(i); Yref = lsim(Pref, Xref, t, 'zoh'), Pref =
+    blkdiag of 1/(50s+1) with iodelay = min over row i of Ps.iodelay (Gs and Ds columns)."""
+    X = np.zeros((7, nit))
+    X[:, tmd - 1: tmd + 5] = SHELL7_YMX[:, None]
+    dl = SHELL7_L.min(axis=1)
+    Y = np.zeros_like(X)
+    for i in range(7):
+        Y[i] = lsim_dtf(c2d_zoh([1.0], [50.0, 1.0], SHELL7_TS, dl[i]), X[i])
+    return Y
+
+
+def shell7x5(nit=SHELL7_NIT):
+    """Return (BandScenario, r = L*Xsp (zeros), v = Rv\\mdv, yref = L*Yref, fixture)."""
+    from .toolbox_band import BandScenario
+
+    fx = load_fixture("shell7x5_14sep2024")
+    L = np.array(fx["scale"]["L"])
+    R = np.array(fx["scale"]["R"])
+    P = shell7x5_plant_scaled(L, R)
+    Ru, Rv = R[:3], R[3:]
+    # MV bounds Shell7x5.m:110-111,135-138 scaled (MPCTuning.m:170-178); no rate bounds
+    umx = 0.5 / Ru
+    inf = np.full(3, np.inf)
+    # OV ScaleFactor = Yrange (Shell7x5.m:162-168); MPCTuning.m:182-184 multiplies by L only
+    # when the factor is not 1 (Yrange = 1 for outputs 3..7 stays 1)
+    yr = 2 * SHELL7_YMX
+    sy = np.where(yr != 1.0, L * yr, yr)
+    su = np.ones(3)                      # Urange = 1 -> unchanged
+    sc = BandScenario(plant=P, nu=3, du_min=-inf, du_max=inf, u_min=-umx, u_max=umx,
+                      y_min=-L * SHELL7_YMX, y_max=L * SHELL7_YMX, ecr_min=SHELL7_ECR.copy(),
+                      ecr_max=SHELL7_ECR.copy(), sy=sy, su=su, rho=1e4)
+    r = np.zeros((7, nit))                                   # L*Xsp, Xsp = 0 (Shell7x5.m:118)
+    mdv = np.zeros((2, nit))
+    mdv[:, 19:] = 0.5                                        # Shell7x5.m:121-123 (1-based 20:end)
+    v = mdv / Rv[:, None]                                    # MPCTuning.m:191
+    yref = L[:, None] * shell7x5_yref(nit)                   # MPCTuning.m:188
+    return sc, r, v, yref, fx
