@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 2 /* 2: DTC-GPC predictor + plant-only disturbances; v1 descriptors accepted */
+#define MPCT_ABI_VERSION 3 /* 3: MD feed-forward + soft output bands; 2: DTC-GPC predictor + plant-only
+                              disturbances + plant variants; v1 and v2 descriptors accepted */
 
 /* error codes */
 #define MPCT_OK 0
@@ -114,6 +115,27 @@ typedef struct mpct_scenario_desc {
    * plant_var  [nplant][my*(nu+nd)] variant plants (replace plant when nplant > 1)           */
   int32_t nplant;
   const mpct_dtf* plant_var;
+  /* ---- abi_version >= 3 --------------------------------------------------------------------
+   * mdband   1: the toolbox MPC with measured-disturbance feed-forward and soft output bands
+   *             (Shell7x5.m:112-196, WoodBerry.m:102-148; mdband_kernel.hip).  MD
+   *             columns nu..nu+nd-1 of plant/model enter the prediction held at v(t)
+   *             (mpcsimopt MDLookAhead 'off'); OV Min/Max are softened by MinECR/MaxECR with ONE
+   *             slack eps >= 0 weighted by rho_ecr (Weights.ECR); Weights.OV / Weights.MVRate act
+   *             over the ScaleFactors.  Requires plant == model (closedloop_toolbox.m:50 sims the
+   *             model), n1[i] == 1 (PredictionHorizon window), dtc == 0, nq == 0, nplant <= 1 and
+   *             nu*nu_max + 1 <= 64.  na/carima_A/nb/carima_B/dp may be NULL (no Diophantine tables).
+   * y_min, y_max [my]      OV Min / Max, already scaled (MPCTuning.m:180-181); +-INFINITY: none
+   * ecr_min, ecr_max [my]  OV MinECR / MaxECR (0: hard output bound)
+   * y_scale [my], u_scale [nu]  OV / MV ScaleFactor after MPCTuning.m:175-184 (NULL: all 1)
+   * rho_ecr                Weights.ECR (Shell7x5.m:191, MPCTuning.m:354)                       */
+  int32_t mdband;
+  const double* y_min;
+  const double* y_max;
+  const double* ecr_min;
+  const double* ecr_max;
+  const double* y_scale;
+  const double* u_scale;
+  double rho_ecr;
 } mpct_scenario_desc;
 
 typedef struct mpct_scenario mpct_scenario;

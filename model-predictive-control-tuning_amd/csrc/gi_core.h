@@ -6,6 +6,28 @@
 
 namespace mpct {
 
+// constraint p = 4*m + kind on move m = n*Nu + l:
+//   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
+//   kind 2:  sum_{l'<=l} du_(n,l') >= u_min - u_prev    kind 3: -sum >= -(u_max - u_prev)
+struct CInfo {
+  int j0, j1;
+  double sg;
+};
+__device__ __forceinline__ CInfo cinfo(int p, int Nu) {
+  const int m = p >> 2, kind = p & 3;
+  CInfo c;
+  c.sg = (kind & 1) ? -1.0 : 1.0;
+  c.j0 = kind < 2 ? m : (m / Nu) * Nu;
+  c.j1 = m;
+  return c;
+}
+
+// per-lane constraint data for QP row m (registers)
+struct RowCons {
+  double dmin, dmax, umin, umax;
+  int n, l;
+};
+
 // Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this
 // family) in its factored, numerically stable form.  H = R'R;  J (M x M) with
 // H^-1 = J J' starts as R^-1; the active normals N_A satisfy J'N_A = [R_A; 0].

@@ -70,28 +70,6 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   return L;
 }
 
-// constraint p = 4*m + kind on move m = n*Nu + l:
-//   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
-//   kind 2:  sum_{l'<=l} du_(n,l') >= u_min - u_prev    kind 3: -sum >= -(u_max - u_prev)
-struct CInfo {
-  int j0, j1;
-  double sg;
-};
-__device__ __forceinline__ CInfo cinfo(int p, int Nu) {
-  const int m = p >> 2, kind = p & 3;
-  CInfo c;
-  c.sg = (kind & 1) ? -1.0 : 1.0;
-  c.j0 = kind < 2 ? m : (m / Nu) * Nu;
-  c.j1 = m;
-  return c;
-}
-
-// per-lane constraint data for QP row m (registers)
-struct RowCons {
-  double dmin, dmax, umin, umax;
-  int n, l;
-};
-
 // slacks of the 4 constraints of row m at x (x in LDS), up = u_prev of the row's MV
 __device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m, const RowCons& rc,
                                            double up, double s[4]) {

@@ -1,0 +1,774 @@
+// mdband_kernel.hip — batched closed loop of the toolbox MPC with measured-disturbance
+// feed-forward and soft output bands, one wavefront (64 lanes) per simulation.
+//
+// Replaces, per simulation, closedloop_toolbox.m:36-100 for an mpc object with measured
+// disturbances (setmpcsignals MV/MD, Shell7x5.m:171-172, WoodBerry.m:102), OV Min/Max softened by
+// MinECR/MaxECR (Shell7x5.m:141-152), ScaleFactors (Shell7x5.m:155-168, rescaled by
+// MPCTuning.m:175-199) and Weights.ECR (Shell7x5.m:191).  Semantics restated in
+// oracle/toolbox_band.py and DESIGN.md §11:
+//   prediction y(t+k|t), k = 1..N2, MVs u(t-1) + cumulative moves (blocked after Nu), MDs held at
+//   v(t) (MDLookAhead 'off'); nominal model, so the toolbox estimator's prediction is exact;
+//   cost sum (w_y/s_y)^2 (r - y)^2 + sum (w_du/s_u)^2 du^2 + rho eps^2;
+//   MV amplitude / rate hard, ymin - eps V s_y <= y <= ymax + eps V s_y, eps >= 0.
+//
+// Free response without a Phi table (Shell 7x5 at N2 = 127 would need ~1.4 MB of it): the window
+// F_t[k] = y(t+1+k | MVs held at u(t-1), MDs held at v(t)) is carried across steps,
+//     F_t[k] = F_{t-1}[k+1] + sum_n s_in(k+2) du_n(t-1) + sum_m s_im(k+1) dv_m(t),
+// and its new last element F_t[N2-1] is one exact step of every model entry's difference equation
+// from that entry's own tail of the window (one lane per entry; the tail gets the same step
+// corrections).  No truncation: the update is exact for any stable or unstable LTI entry.
+// QP on z = [dU; eps] (Mz = M + 1 lanes): H = R'R with R from the row-streamed Givens QR of
+// [Q^1/2 G; Lambda^1/2; rho^1/2 e_eps] (band mode, Q = 0: R is diagonal), g = G'Q(F - r);
+// constraints: 4 box rows per move (gpc_kernel.hip's encoding), eps >= 0 (row M, kind 0) and
+// 2*my*N2 output rows with normals -/+[G_ik, V s]; the warm-started Goldfarb-Idnani method of
+// gi_core.h with general normals staged in LDS and an LDS bitmap of active output rows.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "gi_core.h"
+#include "mpct_dev.h"
+
+namespace mpct {
+
+struct BandLayout {
+  int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, plb, pla,
+      mzb, mza, step, total;
+};
+
+// LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
+// bitmap (zeroed at start)
+__host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2, int M) {
+  const int Mz = M + 1, my = sc.my, nu = sc.nu, nin = sc.nin, ne = sc.ne;
+  BandLayout L;
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
+  L.ri = take(Mz * Mz);
+  L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
+  L.ra = take(Mz * Mz);  // R_A
+  L.dv = take(Mz);       // d = J'n
+  L.nv = take(Mz);       // staged normal n_p
+  L.xc = take(Mz);       // QP iterate
+  L.gv = take(Mz);       // linear term / triangular-solve scratch
+  L.sl = take(4 * Mz);   // box slacks at the unconstrained minimiser
+  L.ob = take(4 * my);   // y_min, y_max, V_min s_y, V_max s_y
+  L.fr = take(2 * my * N2);                // free-response window, double-buffered by t parity
+  L.bits = take((2 * my * N2 + 63) / 64);  // active output rows (32-bit words)
+  L.du = take(nu);                         // du(t-1)
+  L.uprev = take(nu);
+  L.ucum = take(M);
+  L.ye = take(2 * ne);
+  L.yeh = take(2 * ne * kYeHist);
+  L.uring = take(2 * nin * kURing);
+  L.tail = take(ne * kYeHist);  // model entry tails of the window
+  L.sext = take(ne);            // model entry window extensions
+  L.plb = take(ne * sc.pl_maxb);
+  L.pla = take(ne * sc.pl_maxa);
+  L.mzb = take(ne * sc.mz_maxb);
+  L.mza = take(ne * sc.mz_maxa);
+  L.step = take(my * nu * sc.tlen);
+  L.total = (o + 1) & ~1;
+  return L;
+}
+
+// active flags: box rows (p < 4*Mz) in the lanes' act bits, output rows in the LDS bitmap
+struct BandMark {
+  unsigned* bits;
+  int base;
+  template <class St>
+  __device__ __forceinline__ void operator()(St& S, int p, bool on) const {
+    if (p < base) {
+      BoxMark{}(S, p, on);
+    } else if (threadIdx.x == 0) {
+      const int q = p - base;
+      if (on) bits[q >> 5] |= 1u << (q & 31);
+      else bits[q >> 5] &= ~(1u << (q & 31));
+    }
+  }
+};
+
+template <int MAXM>
+__global__ void __launch_bounds__(64, 1)
+    mdband_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
+                              const int* __restrict__ Nuv, const double* __restrict__ deltav,
+                              const double* __restrict__ lambdav, const double* __restrict__ rv,
+                              const double* __restrict__ vv, const DevOpts o, const DevResult out) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x;
+  const long long sim = blockIdx.x;
+  if (sim >= C * nref) return;
+  const long long c = sim / nref;
+  const int kref = (int)(sim - c * nref);
+  const int my = sc.my, nu = sc.nu, nd = sc.nd, nin = sc.nin, nit = sc.nit, ne = sc.ne, tlen = sc.tlen;
+  const int N2 = N2v[c], Nu = Nuv[c];
+  const int M = nu * Nu, Mz = M + 1;
+  const int P = my * N2;
+  int st = 0;
+
+  auto write_nan = [&](int status) __attribute__((always_inline)) {
+    if (lane < my) {
+      if (out.J1) out.J1[sim * my + lane] = NAN;
+      if (out.j21) out.j21[sim * my + lane] = NAN;
+      if (out.j22) out.j22[sim * my + lane] = NAN;
+    }
+    if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = NAN;
+    if (lane == 0) {
+      if (out.status) out.status[sim] = status;
+      if (out.qp_iters) out.qp_iters[sim] = 0;
+    }
+  };
+  if (N2 <= 0) {
+    write_nan(MPCT_ST_SKIPPED_);
+    return;
+  }
+  if (N2 > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N2 || Mz > MAXM) {
+    write_nan(MPCT_ST_BADHORIZON_);
+    return;
+  }
+  const BandLayout L = band_layout(sc, N2, M);
+  double* sRi = lds + L.ri;
+  double* sJT = lds + L.jt;
+  double* sRA = lds + L.ra;
+  double* sd = lds + L.dv;
+  double* snv = lds + L.nv;
+  double* sxc = lds + L.xc;
+  double* sgv = lds + L.gv;
+  double* ssl = lds + L.sl;
+  double* sob = lds + L.ob;
+  double* sfr = lds + L.fr;
+  unsigned* sbits = reinterpret_cast<unsigned*>(lds + L.bits);
+  double* sdu = lds + L.du;
+  double* suprev = lds + L.uprev;
+  double* sucum = lds + L.ucum;
+  double* sye = lds + L.ye;
+  double* syeh = lds + L.yeh;
+  double* sur = lds + L.uring;
+  double* stail = lds + L.tail;
+  double* sext = lds + L.sext;
+  double* splb = lds + L.plb;
+  double* spla = lds + L.pla;
+  double* smzb = lds + L.mzb;
+  double* smza = lds + L.mza;
+  double* sstep = lds + L.step;
+
+  // ------------------------------------------------------------------ prologue
+  for (int e = lane; e < my * nu * tlen; e += kWave) sstep[e] = sc.step[e];
+  for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
+  for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
+  for (int e = lane; e < ne * sc.mz_maxb; e += kWave) smzb[e] = sc.mz_b[e];
+  for (int e = lane; e < ne * sc.mz_maxa; e += kWave) smza[e] = sc.mz_a[e];
+  for (int e = lane; e < 4 * my; e += kWave) sob[e] = sc.obnd[e];
+  for (int e = lane; e < L.plb - L.fr; e += kWave) lds[L.fr + e] = 0.0;
+  const bool row = lane < Mz;  // QP-row lanes: moves 0..M-1, eps at M
+  RowCons rcn;
+  rcn.n = lane < M ? lane / Nu : 0;
+  rcn.l = lane < M ? lane - rcn.n * Nu : 0;
+  rcn.dmin = sc.bnd[rcn.n];
+  rcn.dmax = sc.bnd[nu + rcn.n];
+  rcn.umin = sc.bnd[2 * nu + rcn.n];
+  rcn.umax = sc.bnd[3 * nu + rcn.n];
+  const double* dl = deltav + c * my;
+  const double* lm = lambdav + c * nu;
+  // toolbox weights over scale factors: q_i = (delta_i / s_y,i)^2, w_n = (lambda_n / s_u,n)^2
+  auto qw = [&](int i) __attribute__((always_inline)) -> double {
+    const double w = fabs(dl[i]) * sc.wscale[i];
+    return sc.wsq ? w * w : w;
+  };
+  lds_sync();
+
+  // QR of W = [Q^1/2 G (outputs with q_i > 0); Lambda^1/2; rho^1/2 e_eps] by row-streamed Givens
+  // rotations (lane = column of R); rows of outputs with q_i = 0 are zero and skipped
+  {
+    double rcol[MAXM];
+    {
+      double w0 = 0.0;
+      if (lane < M) {
+        const double ln = fabs(lm[rcn.n]) * sc.wscale[my + rcn.n];
+        w0 = sc.wsq ? ln : sqrt(ln);
+      } else if (lane == M) {
+        w0 = sqrt(sc.rho);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? w0 : 0.0;
+    }
+    for (int i = 0; i < my; ++i) {
+      const double qi = qw(i);
+      if (!(qi > 0.0)) continue;
+      const double sq = sqrt(qi);
+      for (int r = 0; r < N2; ++r) {
+        double w = 0.0;
+        if (lane < M) {
+          const int tt = 1 + r - rcn.l;
+          w = tt >= 0 ? sq * sstep[(i * nu + rcn.n) * tlen + tt] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k) {
+          if (k < M) {  // the eps column never meets a G row
+            const double b = bcast(w, k);
+            const double a = bcast(rcol[k], k);
+            const double rho = sqrt(a * a + b * b);
+            const bool nz = b != 0.0;
+            const double cs = nz ? a / rho : 1.0, sn = nz ? b / rho : 0.0;
+            const double rk = rcol[k];
+            rcol[k] = cs * rk + sn * w;
+            w = -sn * rk + cs * w;
+          }
+        }
+      }
+    }
+    double* sR = sJT;  // R parks in J's region until the QP starts
+    if (row) {
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k)
+        if (k < Mz) sR[k * Mz + lane] = rcol[k];
+    }
+    lds_sync();
+    bool spd = true;
+    for (int k = 0; k < Mz; ++k)
+      if (!(sR[k * Mz + k] > 0.0)) spd = false;
+    if (!spd) {
+      write_nan(MPCT_ST_NONFINITE_);
+      return;
+    }
+    // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
+    if (row) {
+      for (int kk = lane; kk >= 0; --kk) {
+        double a = (kk == lane) ? 1.0 : 0.0;
+        for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * Mz + j] * sRi[j * Mz + lane];
+        sRi[kk * Mz + lane] = a / sR[kk * Mz + kk];
+      }
+      for (int kk = lane + 1; kk < Mz; ++kk) sRi[kk * Mz + lane] = 0.0;
+    }
+    lds_sync();
+  }
+  bool any_q = false;
+  for (int i = 0; i < my; ++i) any_q = any_q || qw(i) > 0.0;
+
+  const double tol = o.feas_tol;
+  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 10 * Mz + 64;
+  long long iters = 0;
+  const double* rr = rv + (long long)kref * my * nit;
+  const double* vvk = vv ? vv + (long long)kref * nd * nit : nullptr;
+  const int base = 4 * Mz;  // first output-row constraint id
+  const BandMark mark{sbits, base};
+  GIState<MAXM> gis;
+  gi_reset<MAXM>(gis);
+
+  // predicted output of row g = i*N2 + k at the iterate in sxc: F[g] + G_g dU
+  auto yhat = [&](const double* F, int g) __attribute__((always_inline)) -> double {
+    const int i = g / N2, k = g - i * N2;
+    double a0 = F[g], a1 = 0.0;
+    const int lmax = min(Nu - 1, k + 1);
+    for (int n = 0; n < nu; ++n) {
+      const double* sp = sstep + (i * nu + n) * tlen + (k + 1);
+      const double* xp = sxc + n * Nu;
+      int l = 0;
+      for (; l + 1 <= lmax; l += 2) {
+        a0 += sp[-l] * xp[l];
+        a1 += sp[-l - 1] * xp[l + 1];
+      }
+      if (l <= lmax) a0 += sp[-l] * xp[l];
+    }
+    return a0 + a1;
+  };
+  // slack of output-row constraint q = 2g + side at the iterate (eps = x_M)
+  auto out_slack = [&](const double* F, int q, double eps) __attribute__((always_inline)) -> double {
+    const int g = q >> 1, i = g / N2;
+    const double yh = yhat(F, g);
+    if (q & 1) return yh - sob[i] + sob[2 * my + i] * eps;        // lower: y + V s eps >= ymin
+    return sob[my + i] + sob[3 * my + i] * eps - yh;              // upper: ymax + V s eps >= y
+  };
+  auto out_active = [&](int q) __attribute__((always_inline)) -> bool { return (sbits[q >> 5] >> (q & 31)) & 1u; };
+  // stage the normal of constraint p in LDS and return this lane's d_k = (J'n_p)_k (also in sd)
+  auto dvec = [&](int p) __attribute__((always_inline)) -> double {
+    const int lpm = __builtin_amdgcn_readlane(rcn.l, p < base ? (p >> 2) : 0);  // uniform
+    if (row) {
+      double nvv = 0.0;
+      if (p < base) {
+        const int m = p >> 2, kind = p & 3;
+        if (m == M) {
+          nvv = lane == M ? 1.0 : 0.0;
+        } else {
+          const int j0 = kind < 2 ? m : m - lpm;
+          nvv = (lane >= j0 && lane <= m) ? ((kind & 1) ? -1.0 : 1.0) : 0.0;
+        }
+      } else {
+        const int q = p - base, g = q >> 1, i = g / N2, k = g - i * N2;
+        if (lane < M) {
+          const int tt = k + 1 - rcn.l;
+          nvv = tt >= 0 ? sstep[(i * nu + rcn.n) * tlen + tt] : 0.0;
+          if (!(q & 1)) nvv = -nvv;
+        } else {
+          nvv = sob[((q & 1) ? 2 : 3) * my + i];
+        }
+      }
+      snv[lane] = nvv;
+    }
+    lds_sync();
+    double dk = 0.0;
+    if (row) {
+      const double* jc = sJT + lane * Mz;
+      double d1 = 0.0;
+      int r = 0;
+      for (; r + 1 < Mz; r += 2) {
+        dk += jc[r] * snv[r];
+        d1 += jc[r + 1] * snv[r + 1];
+      }
+      if (r < Mz) dk += jc[r] * snv[r];
+      dk += d1;
+      sd[lane] = dk;
+    }
+    return dk;
+  };
+
+  // one toolbox QP at the window F, reference r (lane i < my holds r_i), MV u_prev in LDS;
+  // result in sxc (moves 0..M-1, eps at M)
+  auto solve = [&](const double* F, double r_i) __attribute__((always_inline)) {
+    // ---- unconstrained minimiser x_u = -R^-1 R^-T g, g = G'Q(F - r)  (g = 0 in band mode)
+    double xu = 0.0;
+    if (any_q) {
+      if (lane < my) sgv[lane] = r_i;
+      lds_sync();
+      double g = 0.0;
+      if (lane < M) {
+        for (int i = 0; i < my; ++i) {
+          const double qi = qw(i);
+          if (!(qi > 0.0)) continue;
+          const double ri = sgv[i];
+          const double* sp = sstep + (i * nu + rcn.n) * tlen;
+          for (int k = rcn.l > 0 ? rcn.l - 1 : 0; k < N2; ++k) g += qi * sp[k + 1 - rcn.l] * (F[i * N2 + k] - ri);
+        }
+      }
+      lds_sync();
+      if (row) sgv[lane] = g;
+      lds_sync();
+      double y = 0.0;
+      if (row)
+        for (int m = 0; m <= lane; ++m) y += sRi[m * Mz + lane] * sgv[m];
+      lds_sync();
+      if (row) sgv[lane] = y;
+      lds_sync();
+      if (row)
+        for (int k = lane; k < Mz; ++k) xu -= sRi[lane * Mz + k] * sgv[k];
+    }
+    const double up_row = lane < M ? suprev[rcn.n] : 0.0;
+    const double lo_box = fmax(rcn.dmin, rcn.umin - up_row), hi_box = fmin(rcn.dmax, rcn.umax - up_row);
+    auto box_slacks = [&](double x, double s[4]) __attribute__((always_inline)) {
+      const double pre = block_prefix<MAXM>(x, rcn.l, Nu, lane < M, sxc);
+      s[0] = s[1] = s[2] = s[3] = INFINITY;
+      if (lane < M) {
+        if (rcn.l == 0) {
+          s[0] = x - lo_box;
+          s[1] = hi_box - x;
+        } else {
+          s[0] = x - rcn.dmin;
+          s[1] = rcn.dmax - x;
+          s[2] = pre - (rcn.umin - up_row);
+          s[3] = (rcn.umax - up_row) - pre;
+        }
+      } else if (lane == M) {
+        s[0] = x;  // eps >= 0
+      }
+    };
+    // most violated inactive constraint at the iterate x (this lane's component xm)
+    auto most_violated = [&](double xm, double& best, int& bid, double s[4]) __attribute__((always_inline)) {
+      box_slacks(xm, s);
+      if (row) sxc[lane] = xm;
+      lds_sync();
+      best = INFINITY;
+      bid = 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (!((gis.act >> k) & 1u) && s[k] < best) {
+          best = s[k];
+          bid = 4 * lane + k;
+        }
+      const double eps = sxc[M];
+      for (int g = lane; g < P; g += kWave) {
+        const int i = g / N2;
+        const double yh = yhat(F, g);
+        if (isfinite(sob[my + i])) {
+          const int q = 2 * g;
+          const double s_up = sob[my + i] + sob[3 * my + i] * eps - yh;
+          if (s_up < best && !out_active(q)) {
+            best = s_up;
+            bid = base + q;
+          }
+        }
+        if (isfinite(sob[i])) {
+          const int q = 2 * g + 1;
+          const double s_lo = yh - sob[i] + sob[2 * my + i] * eps;
+          if (s_lo < best && !out_active(q)) {
+            best = s_lo;
+            bid = base + q;
+          }
+        }
+      }
+      wave_argmin64(best, bid);
+    };
+    int it = 0;
+    double xm = row ? xu : 0.0;
+    {
+      double best, s[4];
+      int bid;
+      most_violated(xm, best, bid, s);
+      if (!(best < -tol)) return 0;  // x_u feasible: optimal (the retained set is kept)
+      if (gis.q == 0) {
+        gis.jinit = false;
+      } else {
+        if (row) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
+        }
+        lds_sync();
+        if (!gis.jinit || gis.nrot >= 4 * Mz) {
+          // rebuild J (and R_A) for the retained set from R^-1
+          const int qq = gis.q;
+          gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+          gis.q = 0;
+          for (int v = 0; v < qq; ++v) {
+            const int p = __builtin_amdgcn_readlane(gis.ww, v);
+            const double dk = dvec(p);
+            const double beta = qsum<MAXM>(lane >= v && row ? dk * dk : 0.0);
+            lds_sync();
+            const double zm = gi_z(sJT, sd, v, Mz, row);
+            const double uk = gis.uw;
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark);
+            if (lane == v) gis.uw = uk;
+            ++it;
+          }
+          gis.nrot = 0;
+        }
+        lds_sync();
+        // equality-constrained solve on the retained set from x_u, dropping negative multipliers
+        for (;;) {
+          const int q = gis.q;
+          if (q == 0) {
+            xm = row ? xu : 0.0;
+            break;
+          }
+          double cc = 0.0;
+          if (lane < q) {
+            const int p = gis.ww;
+            cc = p < base ? -ssl[p] : -out_slack(F, p - base, sxc[M]);
+          }
+          double wv = 0.0;
+          xm = row ? xu : 0.0;
+          for (int v = 0; v < q; ++v) {  // R_A'w = c, x = x_u + J(:,0:q) w
+            const double w = bcast(cc * gis.rdg, v);
+            if (lane == v) wv = w;
+            if (lane > v && lane < q) cc -= sRA[v * Mz + lane] * w;
+            if (row) xm += sJT[v * Mz + lane] * w;
+          }
+          const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv);
+          if (lane < q) gis.uw = lam;
+          double lmin = lane < q ? lam : INFINITY;
+          int kd = lane;
+          qargmin<MAXM>(lmin, kd);
+          if (!(lmin < 0.0)) break;
+          gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark);
+          ++it;
+        }
+        if (!row) xm = 0.0;
+      }
+    }
+    for (;;) {
+      double best, s[4];
+      int bid;
+      most_violated(xm, best, bid, s);
+      if (!(best < -tol)) break;
+      if (it >= maxit || gis.q >= Mz) {
+        st |= MPCT_ST_QP_MAXITER_;
+        break;
+      }
+      if (!gis.jinit) gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+      const int p = bid;
+      double sp = best, upm = 0.0;
+      bool infeas = false;
+      for (;;) {
+        ++it;
+        const double dk = dvec(p);
+        const double d2 = row ? dk * dk : 0.0;
+        const double dn2 = qsum<MAXM>(d2);
+        const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
+        lds_sync();
+        const double zm = gi_z(sJT, sd, gis.q, Mz, row);
+        const double rk = gi_backsub<MAXM>(gis, sRA, Mz, dk);
+        double t1 = INFINITY;
+        int kdrop = 0x7fffffff;
+        if (lane < gis.q && rk > 0.0) {
+          t1 = gis.uw / rk;
+          kdrop = lane;
+        }
+        qargmin<MAXM>(t1, kdrop);
+        const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
+        if (t1 == INFINITY && t2 == INFINITY) {
+          st |= MPCT_ST_QP_INFEAS_;
+          infeas = true;
+          break;
+        }
+        const bool full = t2 <= t1;
+        const double t = full ? t2 : t1;
+        if (t2 != INFINITY) xm += t * zm;
+        if (lane < gis.q) gis.uw -= t * rk;
+        upm += t;
+        sp += t * beta;
+        if (full) {
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark);
+          break;
+        }
+        gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark);
+        if (it >= maxit) {
+          st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
+      }
+      if (it >= maxit || infeas) break;
+    }
+    if (row) sxc[lane] = xm;
+    lds_sync();
+    return it;
+  };
+
+  // ------------------------------------------------------------------ open-loop prediction
+  // closedloop_toolbox.m:86-91: initial state, yo = 0, reference r(:,end), MD v(:,end) held from
+  // time 0: the window is the MD step responses times v_end
+  double jnu = 0.0;
+  if (o.open_loop) {
+    for (int g = lane; g < P; g += kWave) {
+      const int i = g / N2, k = g - i * N2;
+      double f = 0.0;
+      for (int m = 0; m < nd; ++m) f += sc.step_md[(i * nd + m) * tlen + k + 1] * vvk[m * nit + nit - 1];
+      sfr[g] = f;
+    }
+    lds_sync();
+    iters += solve(sfr, lane < my ? rr[lane * nit + nit - 1] : 0.0);
+    if (lane < M) {
+      double s = 0.0;
+      for (int j = lane - rcn.l; j <= lane; ++j) s += sxc[j];
+      sucum[lane] = s;  // Uopt row l of MV n (held after Nu-1)
+    }
+    lds_sync();
+    if (lane < nu) {
+      // VNS2.m:183-191: Xnu = |uopt(:,1)| ./ |diff(uopt)|, inf/NaN -> 0, Jnu = sum Xnu^2
+      const double u0 = fabs(sucum[lane * Nu]);
+      const int nd_ = Nu - 1 < nit - 1 ? Nu - 1 : nit - 1;
+      for (int t = 0; t < nd_; ++t) {
+        const double dd = fabs(sucum[lane * Nu + t + 1] - sucum[lane * Nu + t]);
+        const double xr = u0 / dd;
+        if (isfinite(xr)) jnu += xr * xr;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ closed loop
+  double j1 = 0.0, j21 = 0.0, j22 = 0.0;
+  const int ncopy = o.open_loop ? 2 : 1;
+  double r_t = 0.0, yr_t = 0.0;
+  if (lane < my) {
+    r_t = rr[lane * nit];
+    yr_t = sc.yref[lane * nit];
+  }
+  for (int t = 0; t < nit; ++t) {
+    double r_n = 0.0, yr_n = 0.0;
+    if (lane < my && t + 1 < nit) {
+      r_n = rr[lane * nit + t + 1];
+      yr_n = sc.yref[lane * nit + t + 1];
+    }
+    // inputs known at t: MDs v(t) (both copies); the open-loop copy's MVs uopt(t)
+    for (int e = lane; e < ncopy * nd; e += kWave) {
+      const int cpy = e / nd, j = e - cpy * nd;
+      sur[(cpy * nin + nu + j) * kURing + (t & (kURing - 1))] = vvk[j * nit + t];
+    }
+    if (o.open_loop && lane < nu) {
+      const int l = t < Nu - 1 ? t : Nu - 1;
+      sur[(nin + lane) * kURing + (t & (kURing - 1))] = sucum[lane * Nu + l];
+    }
+    lds_sync();
+    // plant entries y_e(t) (copy 0 closed loop, copy 1 open loop driven by uopt)
+    for (int e = lane; e < ncopy * ne; e += kWave) {
+      const int cpy = e / ne, ee = e - cpy * ne, j = ee % nin;
+      const double* eb = splb + ee * sc.pl_maxb;
+      const double* ea = spla + ee * sc.pl_maxa;
+      const double* eur = sur + (cpy * nin + j) * kURing;
+      double* eyh = syeh + e * kYeHist;
+      const int nb = sc.pl_nb[ee], na = sc.pl_na[ee], off = sc.pl_off[ee];
+      double a0 = 0.0, a1 = 0.0;
+      for (int l = off; l < nb; ++l) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
+      for (int l = 1; l < na; ++l) a1 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
+      const double acc = a0 + a1;
+      eyh[t & (kYeHist - 1)] = acc;
+      sye[e] = acc;
+    }
+    lds_sync();
+    if (lane < my) {
+      const int i = lane;
+      double y = 0.0;
+      for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
+      const double e1 = y - yr_t;
+      j1 += e1 * e1;
+      if (t >= sc.ink0) j22 += e1 * e1;
+      double ysv = 0.0;
+      if (o.open_loop) {
+        for (int j = 0; j < nin; ++j) ysv += sye[ne + i * nin + j];
+        if (t >= sc.ink0) j21 += (y - ysv) * (y - ysv);
+      }
+      if (o.want_traj) {
+        if (out.y) out.y[(sim * my + i) * nit + t] = y;
+        if (o.open_loop && out.ys) out.ys[(sim * my + i) * nit + t] = ysv;
+      }
+    }
+    // ---- free-response window F_{t-1} -> F_t
+    // model entry tails: step corrections for du(t-1) and dv(t), then one difference-equation
+    // step at tau = t + N2 (MVs u(min(tau', t-1)), MDs v(min(tau', t)))
+    for (int e = lane; e < ne; e += kWave) {
+      const int i = e / nin, j = e - i * nin;
+      const double* mb = smzb + e * sc.mz_maxb;
+      const double* ma = smza + e * sc.mz_maxa;
+      const double* eur = sur + j * kURing;
+      double* tl = stail + e * kYeHist;
+      const int nb = sc.mz_nb[e], na = sc.mz_na[e] - 1, off = sc.mz_off[e];
+      if (j < nu) {
+        const double dlt = sdu[j];
+        if (dlt != 0.0) {
+          const double* sp = sstep + (i * nu + j) * tlen;
+          for (int l = 0; l < na; ++l)
+            if (N2 - l >= 0) tl[l] += sp[N2 - l] * dlt;
+        }
+      } else {
+        const double vt = eur[t & (kURing - 1)];
+        const double dlt = vt - (t > 0 ? eur[(t - 1) & (kURing - 1)] : 0.0);
+        if (dlt != 0.0) {
+          const double* sp = sc.step_md + (i * nd + (j - nu)) * tlen;
+          for (int l = 0; l < na; ++l)
+            if (N2 - 1 - l >= 0) tl[l] += sp[N2 - 1 - l] * dlt;
+        }
+      }
+      const int tcap = j < nu ? t - 1 : t;
+      double a0 = 0.0, a1 = 0.0;
+      for (int l = off; l < nb; ++l) {
+        const int tau = min(t + N2 - l, tcap);
+        if (tau >= 0) a0 += mb[l] * eur[tau & (kURing - 1)];
+      }
+      for (int l = 1; l <= na; ++l) a1 -= ma[l] * tl[l - 1];
+      const double ext = a0 + a1;
+      for (int l = na - 1; l > 0; --l) tl[l] = tl[l - 1];
+      if (na > 0) tl[0] = ext;
+      sext[e] = ext;
+    }
+    lds_sync();
+    const double* Fp = sfr + ((t + 1) & 1) * P;
+    double* Fc = sfr + (t & 1) * P;
+    bool any_dv = false;
+    for (int m = 0; m < nd; ++m) {
+      const double* vr = sur + (nu + m) * kURing;
+      any_dv = any_dv || (vr[t & (kURing - 1)] != (t > 0 ? vr[(t - 1) & (kURing - 1)] : 0.0));
+    }
+    for (int g = lane; g < P; g += kWave) {
+      const int i = g / N2, k = g - i * N2;
+      double f;
+      if (k < N2 - 1) {
+        f = Fp[g + 1];
+        for (int n = 0; n < nu; ++n) f += sstep[(i * nu + n) * tlen + k + 2] * sdu[n];
+        if (any_dv) {
+          for (int m = 0; m < nd; ++m) {
+            const double* vr = sur + (nu + m) * kURing;
+            const double dv = vr[t & (kURing - 1)] - (t > 0 ? vr[(t - 1) & (kURing - 1)] : 0.0);
+            f += sc.step_md[(i * nd + m) * tlen + k + 1] * dv;
+          }
+        }
+      } else {
+        f = 0.0;
+        for (int j = 0; j < nin; ++j) f += sext[i * nin + j];
+      }
+      Fc[g] = f;
+    }
+    lds_sync();
+    iters += solve(Fc, r_t);
+    if (lane < nu) {
+      const int n = lane;
+      const double du = sxc[n * Nu];
+      const double un = suprev[n] + du;
+      sdu[n] = du;
+      sur[n * kURing + (t & (kURing - 1))] = un;
+      if (o.want_traj) {
+        if (out.u) out.u[(sim * nu + n) * nit + t] = un;
+        if (o.open_loop && out.uopt) {
+          const int l = t < Nu - 1 ? t : Nu - 1;
+          out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
+        }
+      }
+      suprev[n] = un;
+    }
+    lds_sync();
+    r_t = r_n;
+    yr_t = yr_n;
+  }
+
+  // ------------------------------------------------------------------ results
+  if (lane < my) {
+    if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;
+    if (out.J1) out.J1[sim * my + lane] = j1;
+    if (out.j22) out.j22[sim * my + lane] = j22;
+    if (out.j21) out.j21[sim * my + lane] = o.open_loop ? j21 : NAN;
+  }
+  if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = o.open_loop ? jnu : NAN;
+  const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
+  if (lane == 0) {
+    const int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
+    if (out.status) out.status[sim] = s;
+    if (out.qp_iters) out.qp_iters[sim] = iters;
+  }
+}
+
+}  // namespace mpct
+
+// ------------------------------------------------------------------------------------------
+// host-side launch
+#include <string>
+
+namespace mpct {
+
+long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu) {
+  const BandLayout L = band_layout(sc, N2, sc.nu * Nu);
+  return (long long)L.total * 8;
+}
+
+template <int MAXM>
+static int launch_band_t(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
+                         const double* delta, const double* lambda, const double* r, const double* v,
+                         const DevOpts& o, const DevResult& out, hipStream_t stream, std::string* err) {
+  const long long lds = mdband_lds_bytes(sc, sc.n2max, sc.numax);
+  if (lds > 160 * 1024) {
+    *err = "scenario needs more than 160 KiB of LDS per simulation";
+    return -4;
+  }
+  auto kern = mdband_closed_loop_kernel<MAXM>;
+  if (lds > 64 * 1024) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess) {
+      *err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed";
+      return -3;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
+                     delta, lambda, r, v, o, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
+    return -3;
+  }
+  return 0;
+}
+
+int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
+                  const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
+                  hipStream_t stream, std::string* err) {
+  const int Mz = sc.nu * sc.numax + 1;
+  if (Mz <= 16) return launch_band_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
+  if (Mz <= 32) return launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
+  if (Mz <= 64) return launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
+  *err = "nu*nu_max + 1 > 64";
+  return -4;
+}
+
+}  // namespace mpct

@@ -63,6 +63,13 @@ struct DevScenario {
   const int* fr_n;      // [my]
   const double* fr_b;   // [my][fr_max]
   const double* fr_a;   // [my][fr_max]
+  // MD feed-forward + soft output bands (mdband = 1, mdband_kernel.hip): the model entries of all
+  // nin = nu + nd columns are the mz_* tables ([my*nin], z^-1 form with delays)
+  int mdband;
+  double rho;             // Weights.ECR
+  const double* step_md;  // [my][nd][tlen]  model MD step responses
+  const double* obnd;     // [4][my]  y_min, y_max, MinECR*s_y, MaxECR*s_y (+-inf: no bound)
+  const double* wscale;   // [my + nu]  1/s_y, 1/s_u (weights over ScaleFactors)
 };
 
 struct DevOpts {

@@ -27,6 +27,11 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
                        hipStream_t stream, std::string* err);
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
+// defined in mdband_kernel.hip
+int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
+                  const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
+                  hipStream_t stream, std::string* err);
+long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu);
 }  // namespace mpct
 
 using namespace mpct;
@@ -60,6 +65,13 @@ struct mpct_scenario {
   std::vector<int> fr_n;
   std::vector<double> bnd;   // [4][nu]
   std::vector<double> yref;  // [my][nit]
+  // MD feed-forward + soft output bands (abi >= 3): model entries of all nin columns in the mz_*
+  // tables, MD step responses, output bounds, weight scales
+  int mdband = 0;
+  double rho = 0.0;
+  std::vector<double> step_md;  // [my][nd][tlen]
+  std::vector<double> obnd;     // [4][my]
+  std::vector<double> wscale;   // [my + nu]
   // device state
   int dev = -2;
   void* dtab = nullptr;
@@ -104,21 +116,27 @@ static void step_response(const mpct_dtf& d, int T, double* s) {
 extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenario** out) {
   if (!d || !out) return fail(MPCT_EINVAL, "null argument");
   *out = nullptr;
-  if (d->abi_version != 1 && d->abi_version != MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
+  if (d->abi_version < 1 || d->abi_version > MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
   const int dtc = d->abi_version >= 2 ? (d->dtc ? 1 : 0) : 0;
   const int nq = d->abi_version >= 2 ? d->nq : 0;
   const int nplant = (d->abi_version >= 2 && d->nplant > 1) ? d->nplant : 1;
+  const int mdband = d->abi_version >= 3 ? (d->mdband ? 1 : 0) : 0;
+  if (mdband && (dtc || nq > 0 || nplant > 1))
+    return fail(MPCT_EINVAL, "mdband excludes dtc, plant-only disturbances and plant variants");
+  if (mdband && (!d->y_min || !d->y_max || !d->ecr_min || !d->ecr_max))
+    return fail(MPCT_EINVAL, "mdband needs y_min, y_max, ecr_min, ecr_max");
   if (nplant > 1 && !d->plant_var) return fail(MPCT_EINVAL, "nplant > 1 needs plant_var");
   if (nq < 0 || (nq > 0 && !d->dist)) return fail(MPCT_EINVAL, "nq > 0 needs dist");
   if (d->my < 1 || d->nu < 1 || d->nd < 0 || d->nit < 1 || d->n2_max < 1 || d->nu_max < 1)
     return fail(MPCT_EINVAL, "non-positive dimension");
   if (d->my > kMaxOut || d->nu + d->nd > kMaxIn) return fail(MPCT_ERANGE, "too many outputs/inputs");
-  if (d->nd > 0)
-    return fail(MPCT_ERANGE, "measured disturbances (nd > 0) are not supported by this build yet");
-  if (d->nu * d->nu_max > 64) return fail(MPCT_ERANGE, "nu*nu_max > 64 (one wavefront of QP rows)");
-  if (!d->n1 || !d->plant || !d->model || !d->na || !d->carima_A || !d->nb || !d->carima_B || !d->dp ||
-      !d->du_min || !d->du_max || !d->u_min || !d->u_max || !d->yref)
+  if (d->nd > 0 && !mdband)
+    return fail(MPCT_ERANGE, "measured disturbances (nd > 0) need the mdband kernel (mdband = 1)");
+  if (d->nu * d->nu_max + mdband > 64) return fail(MPCT_ERANGE, "nu*nu_max (+1 eps row) > 64 (one wavefront of QP rows)");
+  if (!d->n1 || !d->plant || !d->model || !d->du_min || !d->du_max || !d->u_min || !d->u_max || !d->yref)
     return fail(MPCT_EINVAL, "null table pointer");
+  if (!mdband && (!d->na || !d->carima_A || !d->nb || !d->carima_B || !d->dp))
+    return fail(MPCT_EINVAL, "null CARIMA table pointer");
   auto* s = new mpct_scenario();
   s->my = d->my;
   s->nu = d->nu;
@@ -128,6 +146,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   s->nq = nq;
   s->npin = s->nin + nq;
   s->nvar = nplant;
+  s->mdband = mdband;
   if (s->npin > kMaxIn) {
     delete s;
     return fail(MPCT_ERANGE, "too many plant inputs");
@@ -159,6 +178,13 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       }
       step_response(m, s->tlen, &s->step[((size_t)i * nu + n) * s->tlen]);
     }
+  if (mdband) {
+    for (int i = 0; i < my; ++i)
+      if (s->n1[i] != 1) {
+        delete s;
+        return fail(MPCT_EINVAL, "mdband predicts over the toolbox window: n1[i] must be 1");
+      }
+  } else {
   // ---- CARIMA offsets
   std::vector<int> aoff(my + 1, 0), boff(my * nin + 1, 0);
   for (int i = 0; i < my; ++i) {
@@ -286,6 +312,7 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       dst[0] = 1.0;
     }
   }
+  }  // !mdband
   // ---- plant entries in z^-1 form (delay folded into b); plant-only disturbance paths appended
   // as columns nin..npin-1 of each output row
   const int npin = s->npin;
@@ -315,12 +342,12 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
       return fail(MPCT_EINVAL, "plant has direct feedthrough from an MV (algebraic loop)");
     }
   }
-  for (int n = 0; n < nu; ++n)
+  for (int n = 0; n < (mdband ? 0 : nu); ++n)
     if (s->dum[n] > kMaxDum) {
       delete s;
       return fail(MPCT_ERANGE, "past-control register longer than the device supports (16)");
     }
-  for (int i = 0; i < my; ++i)
+  for (int i = 0; i < (mdband ? 0 : my); ++i)
     if (s->nyhi[i] > kYeHist) {
       delete s;
       return fail(MPCT_ERANGE, "CARIMA denominator order too high for the device (na <= 7)");
@@ -407,6 +434,80 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
         s->fr_b[(size_t)i * s->fr_max + q2] = f.num[q2] / f.den[0];
         s->fr_a[(size_t)i * s->fr_max + q2] = f.den[q2] / f.den[0];
       }
+    }
+  }
+  if (mdband) {
+    // the model of every column (MV and MD), z^-1 form with its delay: the window extension
+    // (mdband_kernel.hip); plant == model (closedloop_toolbox.m:50 sims the controller's model)
+    const int nm = my * nin;
+    s->mz_nb.resize(nm);
+    s->mz_na.resize(nm);
+    s->mz_off.resize(nm);
+    for (int e = 0; e < nm; ++e) {
+      const mpct_dtf& m = d->model[e];
+      const mpct_dtf& p = d->plant[e];
+      if (m.len < 1 || !m.num || !m.den || m.den[0] == 0.0 || m.delay < 0) {
+        delete s;
+        return fail(MPCT_EINVAL, "bad model entry");
+      }
+      bool same = p.len == m.len && p.delay == m.delay;
+      for (int k = 0; same && k < m.len; ++k) same = p.num[k] == m.num[k] && p.den[k] == m.den[k];
+      if (!same) {
+        delete s;
+        return fail(MPCT_ERANGE, "mdband: plant must equal the model (the toolbox estimator is not restated)");
+      }
+      s->mz_nb[e] = m.delay + m.len;
+      s->mz_na[e] = m.len;
+      s->mz_maxb = std::max(s->mz_maxb, s->mz_nb[e]);
+      s->mz_maxa = std::max(s->mz_maxa, s->mz_na[e]);
+    }
+    if (s->mz_maxb > kMaxTaps || s->mz_maxa > kYeHist) {
+      delete s;
+      return fail(MPCT_ERANGE, "mdband: model entry too long for the device history rings");
+    }
+    s->mz_b.assign((size_t)nm * s->mz_maxb, 0.0);
+    s->mz_a.assign((size_t)nm * s->mz_maxa, 0.0);
+    for (int e = 0; e < nm; ++e) {
+      const mpct_dtf& m = d->model[e];
+      for (int q2 = 0; q2 < m.len; ++q2) {
+        s->mz_b[(size_t)e * s->mz_maxb + m.delay + q2] = m.num[q2] / m.den[0];
+        s->mz_a[(size_t)e * s->mz_maxa + q2] = m.den[q2] / m.den[0];
+      }
+      int o2 = 0;
+      while (o2 < s->mz_nb[e] && s->mz_b[(size_t)e * s->mz_maxb + o2] == 0.0) ++o2;
+      s->mz_off[e] = o2;
+    }
+    const int nd = s->nd;
+    s->step_md.assign((size_t)my * std::max(nd, 1) * s->tlen, 0.0);
+    for (int i = 0; i < my; ++i)
+      for (int j = 0; j < nd; ++j)
+        step_response(d->model[i * nin + nu + j], s->tlen, &s->step_md[((size_t)i * nd + j) * s->tlen]);
+    s->obnd.assign(4 * my, 0.0);
+    s->wscale.assign(my + nu, 1.0);
+    for (int i = 0; i < my; ++i) {
+      const double sy = d->y_scale ? d->y_scale[i] : 1.0;
+      if (!(sy > 0.0) || !(d->ecr_min[i] >= 0.0) || !(d->ecr_max[i] >= 0.0) || !(d->y_min[i] <= d->y_max[i])) {
+        delete s;
+        return fail(MPCT_EINVAL, "mdband: bad output bound / ECR / scale factor");
+      }
+      s->obnd[i] = d->y_min[i];
+      s->obnd[my + i] = d->y_max[i];
+      s->obnd[2 * my + i] = d->ecr_min[i] * sy;
+      s->obnd[3 * my + i] = d->ecr_max[i] * sy;
+      s->wscale[i] = 1.0 / sy;
+    }
+    for (int n = 0; n < nu; ++n) {
+      const double su = d->u_scale ? d->u_scale[n] : 1.0;
+      if (!(su > 0.0)) {
+        delete s;
+        return fail(MPCT_EINVAL, "mdband: bad MV scale factor");
+      }
+      s->wscale[my + n] = 1.0 / su;
+    }
+    s->rho = d->rho_ecr;
+    if (!(s->rho > 0.0)) {
+      delete s;
+      return fail(MPCT_EINVAL, "mdband: rho_ecr must be > 0");
     }
   }
   s->bnd.resize(4 * nu);
@@ -510,6 +611,9 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   size_t o_frn = put(s->fr_n.data(), s->fr_n.size() * 4);
   size_t o_frb = put(s->fr_b.data(), s->fr_b.size() * 8);
   size_t o_fra = put(s->fr_a.data(), s->fr_a.size() * 8);
+  size_t o_smd = put(s->step_md.data(), s->step_md.size() * 8);
+  size_t o_obnd = put(s->obnd.data(), s->obnd.size() * 8);
+  size_t o_wsc = put(s->wscale.data(), s->wscale.size() * 8);
   void* dp = nullptr;
   if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
   if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -535,10 +639,10 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
   {
-    bool rp = s->pl_maxa - 1 <= kRegA;
+    bool rp = !s->mdband && s->pl_maxa - 1 <= kRegA;  // gpc_kernel.hip only
     for (int e = 0; e < s->nvar * s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
-    for (int n = 0; n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
-    for (int i = 0; i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
+    for (int n = 0; rp && n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
+    for (int i = 0; rp && i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
     ds.regpath = rp ? 1 : 0;
   }
   ds.step = reinterpret_cast<const double*>(b + o_step);
@@ -568,6 +672,11 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.fr_n = reinterpret_cast<const int*>(b + o_frn);
   ds.fr_b = reinterpret_cast<const double*>(b + o_frb);
   ds.fr_a = reinterpret_cast<const double*>(b + o_fra);
+  ds.mdband = s->mdband;
+  ds.rho = s->rho;
+  ds.step_md = reinterpret_cast<const double*>(b + o_smd);
+  ds.obnd = reinterpret_cast<const double*>(b + o_obnd);
+  ds.wscale = reinterpret_cast<const double*>(b + o_wsc);
   s->dtab = dp;
   s->dev = dev;
   return MPCT_OK;
@@ -614,8 +723,10 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   dr.prof = dprof;
 #endif
   std::string err;
-  rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
-                          static_cast<hipStream_t>(stream), &err);
+  rc = s->mdband ? launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr,
+                                 static_cast<hipStream_t>(stream), &err)
+                 : launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
+                                      static_cast<hipStream_t>(stream), &err);
   if (rc) return fail(rc, err);
 #ifdef MPCT_PROFILE
   {
@@ -733,5 +844,6 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.mz_maxb = s->mz_maxb;
   ds.mz_maxa = s->mz_maxa;
   ds.fr_max = s->fr_max;
-  return lds_bytes_for(ds, N2, Nu);
+  ds.mdband = s->mdband;
+  return s->mdband ? mdband_lds_bytes(ds, N2, Nu) : lds_bytes_for(ds, N2, Nu);
 }

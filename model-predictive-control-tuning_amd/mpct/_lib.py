@@ -46,6 +46,11 @@ class MpctScenarioDesc(C.Structure):
         ("dist", C.POINTER(MpctDtf)),
         ("nplant", C.c_int32),
         ("plant_var", C.POINTER(MpctDtf)),
+        ("mdband", C.c_int32),
+        ("y_min", c_double_p), ("y_max", c_double_p),
+        ("ecr_min", c_double_p), ("ecr_max", c_double_p),
+        ("y_scale", c_double_p), ("u_scale", c_double_p),
+        ("rho_ecr", C.c_double),
     ]
 
 
@@ -65,7 +70,7 @@ EXPORTS = [
     "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
 ]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 ST_QP_MAXITER, ST_QP_INFEAS, ST_NONFINITE, ST_SKIPPED, ST_BADHORIZON = 1, 2, 4, 8, 16
 
 _lib = None

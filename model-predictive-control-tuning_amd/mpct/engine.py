@@ -35,11 +35,15 @@ class Scenario:
     delta/lambda).  ``plant``/``model`` are my x (nu+nd) lists of :class:`Tf` (scaled, discrete:
     MPCTuning.m:162 Pze = L*Pz*R).  ``window``: 'toolbox' predicts t+1..t+N2 (PredictionHorizon
     semantics, closedloop_toolbox.m:38), 'gpc' predicts t+dmin+1..t+dmin+N2 (MatG.m / DTC_GPC_WW).
-    ``exact_carima``: exact LCM (toolbox-equivalent) vs BA_MIMO's rounded roots."""
+    ``exact_carima``: exact LCM (toolbox-equivalent) vs BA_MIMO's rounded roots.
+    ``bands``: the toolbox MPC with measured disturbances and soft output bands (Shell7x5.m,
+    WoodBerry.m; ABI mdband): dict(y_min, y_max, ecr_min, ecr_max, y_scale=None, u_scale=None,
+    rho=1e4) of OV Min/Max, MinECR/MaxECR, ScaleFactors and Weights.ECR.  Scenarios with measured
+    disturbances (nd > 0) always use that kernel (unbounded outputs when bands is None)."""
 
     def __init__(self, plant, model, nu, du_min, du_max, u_min, u_max, yref, n2_max, nu_max,
                  Ts=1.0, window="toolbox", weights_squared=True, exact_carima=True, vns_ink=10,
-                 dtc=False, filters=None, dist=None, plant_variants=None):
+                 dtc=False, filters=None, dist=None, plant_variants=None, bands=None):
         self.lib = _lib.load()
         self.plant, self.model = plant, model
         self.my, self.nin = len(model), len(model[0])
@@ -133,6 +137,27 @@ class Scenario:
             keep.append(varr)
             d.nplant = len(plant_variants)
             d.plant_var = varr
+        self.mdband = bands is not None or self.nd > 0
+        if self.mdband:
+            if window != "toolbox" or self.dtc:
+                raise ValueError("the MD / output-band kernel predicts over the toolbox window (no DTC)")
+            b = dict(bands or {})
+            inf = np.full(self.my, np.inf)
+
+            def vec(key, default, n):
+                v = b.get(key)
+                return np.ascontiguousarray(np.broadcast_to(np.asarray(default if v is None else v, dtype=float), (n,)))
+
+            self.bands = {k: vec(k, dflt, n) for k, dflt, n in (
+                ("y_min", -inf, self.my), ("y_max", inf, self.my), ("ecr_min", 1.0, self.my),
+                ("ecr_max", 1.0, self.my), ("y_scale", 1.0, self.my), ("u_scale", 1.0, self.nu))}
+            self.rho = float(b.get("rho", 1e4))
+            keep.extend(self.bands.values())
+            d.mdband = 1
+            d.y_min, d.y_max = _dp(self.bands["y_min"]), _dp(self.bands["y_max"])
+            d.ecr_min, d.ecr_max = _dp(self.bands["ecr_min"]), _dp(self.bands["ecr_max"])
+            d.y_scale, d.u_scale = _dp(self.bands["y_scale"]), _dp(self.bands["u_scale"])
+            d.rho_ecr = self.rho
         h = C.c_void_p()
         rc = self.lib.mpct_scenario_create(C.byref(d), C.byref(h))
         if rc != 0:

@@ -170,3 +170,29 @@ def shell7x5(nit=SHELL7_NIT):
     v = mdv / Rv[:, None]                                    # MPCTuning.m:191
     yref = L[:, None] * shell7x5_yref(nit)                   # MPCTuning.m:188
     return sc, r, v, yref, fx
+
+
+# ---------------------------------------------------------------------------------------------
+# WoodBerry.m toolbox MPC (caso 1, nominal, rest): one measured disturbance, no output bounds.
+# No committed WoodBerry .mat: CondMin's scaling is not pinned, L = R = I.
+WB_K = np.array([[12.8, -18.9, 3.8], [6.6, -19.4, 4.9]])          # WoodBerry.m:48-52
+WB_TAU = np.array([[16.7, 21.0, 14.9], [10.9, 14.4, 13.2]])
+WB_L = np.array([[1.0, 2.0, 8.1], [2.0, 1.0, 3.4]])
+
+
+def woodberry_toolbox(nit=400):
+    """Return (BandScenario, r, v, yref) of WoodBerry.m:43-148 (see mpct.scenarios)."""
+    from .toolbox_band import BandScenario
+
+    P = [[c2d_zoh([WB_K[i, j]], [WB_TAU[i, j], 1.0], 1.0, WB_L[i, j]) for j in range(3)] for i in range(2)]
+    inf = np.full(2, np.inf)
+    sc = BandScenario(plant=P, nu=2, du_min=np.full(2, -0.05), du_max=np.full(2, 0.05),
+                      u_min=np.full(2, -0.5), u_max=np.full(2, 0.5), y_min=-inf, y_max=inf,
+                      ecr_min=np.ones(2), ecr_max=np.ones(2), sy=np.ones(2), su=np.ones(2), rho=1e4)
+    X = np.zeros((2, nit))
+    X[0, 9:] = 0.8
+    X[1, 199:] = 0.5
+    Y = np.stack([lsim_dtf(c2d_zoh([1.0], [tau, 1.0], 1.0, 1.0), X[i]) for i, tau in enumerate((10.0, 7.0))])
+    v = np.zeros((1, nit))
+    v[0, 299:] = -0.25
+    return sc, X, v, Y

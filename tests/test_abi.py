@@ -35,7 +35,7 @@ def test_header_and_exports_agree(built):
 def test_abi_version(built):
     from mpct import _lib
 
-    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_abi_v1_descriptor_accepted(built, monkeypatch):
@@ -48,6 +48,31 @@ def test_abi_v1_descriptor_accepted(built, monkeypatch):
     monkeypatch.setattr(_lib, "ABI_VERSION", 1)
     sc, r, yref = shell3x3(n2_max=10, nu_max=2)
     assert sc.dims()["nx"] == 35
+
+
+def test_mdband_scenario(built, monkeypatch):
+    """Shell 7x5 (config 3) builds the MD / soft-band scenario: its MV step table equals the
+    oracle's step responses of the fixture-pinned plant, the largest search horizon (N2 = 127,
+    Nu = 15: 46 QP rows) fits one workgroup's LDS, and a v2 descriptor (no mdband field) with
+    measured disturbances is refused loudly."""
+    from mpct import _lib
+    from mpct.engine import MpctError
+    from mpct.scenarios import shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import step_table
+
+    sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
+    d = sc.dims()
+    assert (d["my"], d["nu"], d["nd"], d["n2_max"]) == (7, 3, 2, 127)
+    osc = o_shell7x5()[0]
+    S = step_table(osc, d["tlen"])
+    np.testing.assert_allclose(sc.table(0).reshape(7, 3, d["tlen"]), S[:, :3], rtol=1e-13, atol=1e-15)
+    assert sc.lds_bytes(127, 15) <= 160 * 1024
+    with pytest.raises(MpctError, match="eps row"):
+        shell7x5(nu_max=22)                       # 3*22 + 1 QP rows > 64
+    monkeypatch.setattr(_lib, "ABI_VERSION", 2)
+    with pytest.raises(MpctError, match="nd > 0"):
+        shell7x5(n2_max=10, nu_max=2)
 
 
 @pytest.fixture(scope="module")
@@ -118,10 +143,12 @@ def test_errors_are_reported(built):
     yref = np.zeros((3, 50))
     kw = dict(du_min=-0.05 / SHELL3_R, du_max=0.05 / SHELL3_R, u_min=-1.0 / SHELL3_R,
               u_max=0.5 / SHELL3_R, yref=yref, n2_max=30, nu_max=5)
-    # measured disturbances (nd > 0) are not on this round's kernel path: ERANGE, loudly
+    # measured disturbances run on the mdband kernel, which restates the nominal toolbox loop
+    # (plant == model, closedloop_toolbox.m:50): a mismatched plant is refused with ERANGE
     Pd = [row + [c2d([1.0], [10.0, 1.0], 4.0, 4.0)] for row in P]
-    with pytest.raises(MpctError, match=r"\(-4\)"):
-        Scenario(Pd, Pd, nu=3, **kw)
+    Pm = [row[:3] + [c2d([2.0], [10.0, 1.0], 4.0, 4.0)] for row in Pd]
+    with pytest.raises(MpctError, match=r"\(-4\).*plant must equal"):
+        Scenario(Pm, Pd, nu=3, **kw)
     # bounds that exclude 0 are rejected (du = 0 must be feasible at rest)
     bad = dict(kw, du_min=0.01 * np.ones(3))
     with pytest.raises(MpctError):
@@ -180,7 +207,11 @@ def test_kernel_isa_invariants(built):
     size class (M <= 16) must also run without scratch and at 2 waves/SIMD (<= 256 VGPRs)."""
     import __graft_entry__ as g
 
-    text = open(g.kernel_isa()).read()
+    paths = g.kernel_isa()
+    for p in paths:
+        t = open(p).read()
+        assert "s_swappc_b64" not in t and "flat_load" not in t and "flat_store" not in t, p
+    text = open(paths[0]).read()
     assert "s_swappc_b64" not in text
     assert "flat_load" not in text and "flat_store" not in text
     meta = _kernel_meta(text)

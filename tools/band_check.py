@@ -1,0 +1,70 @@
+"""Quick GPU-vs-oracle check of the MD / soft-band kernel (Shell 7x5, WoodBerry toolbox)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "model-predictive-control-tuning_amd")]
+import torch  # noqa: E402,F401  (one HIP runtime: torch's)
+
+from mpct.engine import eval_batch  # noqa: E402
+from mpct.scenarios import SHELL7_TUNED, shell7x5, woodberry_toolbox  # noqa: E402
+from oracle.scenarios import shell7x5 as o_shell7x5, woodberry_toolbox as o_wb  # noqa: E402
+from oracle.toolbox_band import closedloop_band  # noqa: E402
+
+
+def cmp(name, sc, osc, r, v, cands, nit, open_loop=True):
+    N2 = np.array([c[0] for c in cands], np.int32)
+    Nu = np.array([c[1] for c in cands], np.int32)
+    D = np.array([c[2] for c in cands])
+    Lm = np.array([c[3] for c in cands])
+    t0 = time.time()
+    res = eval_batch(sc, N2, Nu, D, Lm, r[None], v=v[None], open_loop=open_loop, want_traj=True, device=0)
+    tg = time.time() - t0
+    worst = 0.0
+    for k, c in enumerate(cands):
+        t1 = time.time()
+        o = closedloop_band(osc, r, v, int(c[0]), int(c[1]), c[2], c[3], nit, open_loop=open_loop)
+        to = time.time() - t1
+        sy = np.abs(o.y).max() + 1e-30
+        su = np.abs(o.u).max() + 1e-30
+        ey = np.abs(res.y[k] - o.y).max() / sy
+        eu = np.abs(res.u[k] - o.u).max() / su
+        msg = "%s cand %d N2=%d Nu=%d st=%d it=%d  y %.2e u %.2e" % (name, k, c[0], c[1], res.status[k], res.qp_iters[k], ey, eu)
+        if open_loop:
+            ey2 = np.abs(res.ys[k] - o.ys).max() / (np.abs(o.ys).max() + 1e-30)
+            eu2 = np.abs(res.uopt[k] - o.uopt).max() / (np.abs(o.uopt).max() + 1e-30)
+            msg += " ys %.2e uopt %.2e" % (ey2, eu2)
+            worst = max(worst, ey2, eu2)
+        print(msg + "  (oracle %.2fs)" % to, flush=True)
+        worst = max(worst, ey, eu)
+    print("%s: gpu %.3fs, worst rel %.3e" % (name, tg, worst), flush=True)
+    return worst
+
+
+def main():
+    rng = np.random.default_rng(7)
+    sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    print("signals:", np.abs(r - orr).max(), np.abs(v - ov).max(), np.abs(yref - oyref).max())
+    cands = [(27, 2, np.zeros(7), np.array(SHELL7_TUNED["lam"]))]
+    for _ in range(5):
+        cands.append((int(rng.integers(5, 41)), int(rng.integers(1, 9)), np.zeros(7), 10 ** rng.uniform(-3, 1, 3)))
+    for _ in range(2):
+        d = np.concatenate([np.zeros(2), 10 ** rng.uniform(-2, 0, 5)])
+        cands.append((int(rng.integers(5, 41)), int(rng.integers(1, 9)), d, 10 ** rng.uniform(-3, 1, 3)))
+    cands = [c for c in cands if c[1] <= c[0]]
+    w1 = cmp("shell7x5", sc, osc, r, v, cands, 200)
+    sc2, r2, v2, y2 = woodberry_toolbox()
+    o2, or2, ov2, oy2 = o_wb()
+    c2 = [(int(rng.integers(5, 31)), int(rng.integers(1, 11)), 10 ** rng.uniform(-2, 0, 2), 10 ** rng.uniform(-3, 0, 2))
+          for _ in range(4)]
+    c2 = [c for c in c2 if c[1] <= c[0]]
+    w2 = cmp("woodberry", sc2, o2, r2, v2, c2, 400)
+    print("WORST", max(w1, w2))
+
+
+if __name__ == "__main__":
+    main()
