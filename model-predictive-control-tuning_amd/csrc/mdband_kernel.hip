@@ -252,6 +252,9 @@ __global__ void __launch_bounds__(64, 1)
   const BandMark mark{sbits, base};
   GIState<MAXM> gis;
   gi_reset<MAXM>(gis);
+#ifdef MPCT_DEBUG_BAND
+  int dbg_t = -1;
+#endif
 
   // predicted output of row g = i*N2 + k at the iterate in sxc: F[g] + G_g dU
   auto yhat = [&](const double* F, int g) __attribute__((always_inline)) -> double {
@@ -369,8 +372,10 @@ __global__ void __launch_bounds__(64, 1)
         s[0] = x;  // eps >= 0
       }
     };
-    // most violated inactive constraint at the iterate x (this lane's component xm)
-    auto most_violated = [&](double xm, double& best, int& bid, double s[4]) __attribute__((always_inline)) {
+    // most violated constraint at the iterate x (this lane's component xm); all_rows: include the
+    // active set (the entry test of x_u, which the retained set does not constrain)
+    auto most_violated = [&](double xm, double& best, int& bid, double s[4], bool all_rows)
+                             __attribute__((always_inline)) {
       box_slacks(xm, s);
       if (row) sxc[lane] = xm;
       lds_sync();
@@ -378,7 +383,7 @@ __global__ void __launch_bounds__(64, 1)
       bid = 0x7fffffff;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (!((gis.act >> k) & 1u) && s[k] < best) {
+        if ((all_rows || !((gis.act >> k) & 1u)) && s[k] < best) {
           best = s[k];
           bid = 4 * lane + k;
         }
@@ -389,7 +394,7 @@ __global__ void __launch_bounds__(64, 1)
         if (isfinite(sob[my + i])) {
           const int q = 2 * g;
           const double s_up = sob[my + i] + sob[3 * my + i] * eps - yh;
-          if (s_up < best && !out_active(q)) {
+          if (s_up < best && (all_rows || !out_active(q))) {
             best = s_up;
             bid = base + q;
           }
@@ -397,7 +402,7 @@ __global__ void __launch_bounds__(64, 1)
         if (isfinite(sob[i])) {
           const int q = 2 * g + 1;
           const double s_lo = yh - sob[i] + sob[2 * my + i] * eps;
-          if (s_lo < best && !out_active(q)) {
+          if (s_lo < best && (all_rows || !out_active(q))) {
             best = s_lo;
             bid = base + q;
           }
@@ -410,7 +415,11 @@ __global__ void __launch_bounds__(64, 1)
     {
       double best, s[4];
       int bid;
-      most_violated(xm, best, bid, s);
+      most_violated(xm, best, bid, s, true);
+#ifdef MPCT_DEBUG_BAND
+      if (sim == 0 && lane == 0 && dbg_t < MPCT_DEBUG_BAND)
+        printf("  entry t=%d best=%.3e bid=%d q=%d xu0=%.9e xuNu=%.9e\n", dbg_t, best, bid, gis.q, sxc[0], sxc[Nu]);
+#endif
       if (!(best < -tol)) return 0;  // x_u feasible: optimal (the retained set is kept)
       if (gis.q == 0) {
         gis.jinit = false;
@@ -474,9 +483,10 @@ __global__ void __launch_bounds__(64, 1)
     for (;;) {
       double best, s[4];
       int bid;
-      most_violated(xm, best, bid, s);
+      most_violated(xm, best, bid, s, false);
       if (!(best < -tol)) break;
-      if (it >= maxit || gis.q >= Mz) {
+      // a full active set (q == Mz) is legal here: beta = 0 forces dual steps (drops) first
+      if (it >= maxit) {
         st |= MPCT_ST_QP_MAXITER_;
         break;
       }
@@ -683,7 +693,16 @@ __global__ void __launch_bounds__(64, 1)
       Fc[g] = f;
     }
     lds_sync();
+#ifdef MPCT_DEBUG_BAND
+    dbg_t = t;
+    const int it_dbg = solve(Fc, r_t);
+    iters += it_dbg;
+    if (sim == 0 && lane == 0 && t < MPCT_DEBUG_BAND)
+      printf("t=%d it=%d q=%d eps=%.9e du=%.9e %.9e %.9e F0=%.9e Fend=%.9e y6=%.9e st=%d\n", t, it_dbg, gis.q,
+             sxc[M], sxc[0], sxc[Nu], sxc[2 * Nu], Fc[0], Fc[N2 - 1], Fc[6 * N2], st);
+#else
     iters += solve(Fc, r_t);
+#endif
     if (lane < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];

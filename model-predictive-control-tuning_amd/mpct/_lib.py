@@ -7,7 +7,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-_CANDIDATES = [
+_CANDIDATES = ([os.environ["MPCT_LIB"]] if os.environ.get("MPCT_LIB") else []) + [
     os.path.join(_PKG, "csrc", "libmpct.so"),
     os.path.join(_HERE, "libmpct.so"),
 ]

@@ -157,7 +157,10 @@ def qp_primal_active_set_x0(W, c, Ain, bin_, x0, tol=1e-12, maxit=2000):
             return x, it, W_
         grad = W.T @ (W @ x + c)
         mu = np.linalg.lstsq(Ain[W_].T, grad, rcond=None)[0]
-        if np.all(mu >= -1e-9 * np.max(np.abs(mu))):
+        # absolute test against the (equilibrated) gradient: on Shell 7x5 the multipliers of the
+        # rows that hold eps span ~1e8 while a wrong working set shows as mu ~ -1e-1, which any
+        # test relative to max|mu| accepts
+        if np.all(mu >= -1e-10 * max(1.0, np.max(np.abs(grad)))):
             return x, it, W_
         W_.pop(int(np.argmin(mu)))
     raise RuntimeError("primal active set did not converge")
@@ -204,16 +207,25 @@ def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     x0 = np.zeros(M + 1)
     viol = b - A @ x0
     need = (viol > 0) & (A[:, M] > 0)
-    if np.any((viol > 0) & ~(A[:, M] > 0)):
+    # hard rows (MV bounds, eps >= 0, ECR-0 outputs) hold at dU = 0 up to the rounding of u_prev
+    # (and, in replay_moves, up to the device QP's feasibility tolerance 1e-10)
+    if np.any((viol > 1e-9 * np.maximum(1.0, np.abs(b))) & ~(A[:, M] > 0)):
         raise NotImplementedError("hard output constraint violated by the free response")
     if np.any(need):
         x0[M] = np.max(viol[need] / A[need, M]) * (1 + 1e-12)
-    x, it, _ = qp_primal_active_set_x0(W, c, A, b, x0)
-    return x, it
+    # equilibrate: rho*eps dominates the gradient by ~9 orders of magnitude over lambda^2*du on
+    # Shell 7x5, which makes any multiplier-sign test relative to max|mu| accept wrong working
+    # sets.  Solve in y = D^-1 x with D = diag(H)^-1/2 and unit-norm constraint rows.
+    dsc = 1.0 / np.sqrt(np.sum(W * W, axis=0))
+    As = A * dsc[None, :]
+    rn = np.linalg.norm(As, axis=1)
+    rn[rn == 0] = 1.0
+    y, it, _ = qp_primal_active_set_x0(W * dsc[None, :], c, As / rn[:, None], b / rn, x0 / dsc)
+    return y * dsc, it
 
 
 def closedloop_band(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, nit: int,
-                    open_loop: bool = True) -> CLResult:
+                    open_loop: bool = True, trace=None) -> CLResult:
     """[y,u,t,ys,uopt] = closedloop_toolbox(mpc,r,v,N,Nu,delta,lambda,nit) restated for the
     band-mode / measured-disturbance configuration.  r: my x nit, v: nd x nit."""
     my, nu, nd, nin = sc.my, sc.nu, sc.nd, sc.nin
@@ -261,6 +273,8 @@ def closedloop_band(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, nit: i
     for t in range(nit):
         Y[:, t] = simulate(ba, U, t + 1)[:, t]
         f = free(U, t, u_prev, v[:, t])
+        if trace is not None:
+            trace.append(f.copy())
         x, it = band_qp(sc, G, f, r[:, t], u_prev, N2, Nu, wq, wl)
         iters += it
         du = np.array([x[n * Nu] for n in range(nu)])
@@ -271,3 +285,38 @@ def closedloop_band(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, nit: i
     res = CLResult(Y, U[:nu, :nit].copy(), ys, uopt, iters, DU)
     res.eps = EPS
     return res
+
+
+def replay_moves(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, U, T=None):
+    """Per-step optimality check of an applied MV trajectory U (nu x nit, e.g. the device's):
+    at every step t the state is rebuilt from U[:, :t] and v, and the toolbox QP is solved there.
+    Returns (du_oracle, du_applied), both nu x T.  A trajectory that diverges from the oracle's
+    free run (unstable or switching closed loops amplify rounding) must still take the QP's
+    optimal move at the state it is actually in."""
+    my, nu, nd, nin = sc.my, sc.nu, sc.nd, sc.nin
+    nit = U.shape[1]
+    T = nit if T is None else T
+    r = np.asarray(r, dtype=float).reshape(my, nit)
+    v = np.asarray(v, dtype=float).reshape(nd, nit)
+    delta = np.abs(np.asarray(delta, dtype=float))
+    lam = np.abs(np.asarray(lam, dtype=float))
+    wq = (delta / sc.sy) ** 2 if sc.weights_squared else delta / sc.sy
+    wl = (lam / sc.su) ** 2 if sc.weights_squared else lam / sc.su
+    ba = sc.ba()
+    G = dyn_matrix(step_table(sc, N2 + 2), nu, N2, Nu)
+    Uall = np.zeros((nin, nit + N2 + 1))
+    Uall[:nu, :nit] = U
+    Uall[nu:, :nit] = v
+    du_o = np.zeros((nu, T))
+    du_a = np.zeros((nu, T))
+    for t in range(T):
+        u_prev = U[:, t - 1] if t > 0 else np.zeros(nu)
+        Uf = np.zeros((nin, t + N2 + 1))
+        Uf[:, :t] = Uall[:, :t]
+        Uf[:nu, t:] = u_prev[:, None]
+        Uf[nu:, t:] = v[:, t][:, None]
+        f = simulate(ba, Uf, t + N2 + 1)[:, t + 1:].reshape(-1)
+        x, _ = band_qp(sc, G, f, r[:, t], u_prev, N2, Nu, wq, wl)
+        du_o[:, t] = [x[n * Nu] for n in range(nu)]
+        du_a[:, t] = U[:, t] - u_prev
+    return du_o, du_a

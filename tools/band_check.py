@@ -12,7 +12,7 @@ import torch  # noqa: E402,F401  (one HIP runtime: torch's)
 from mpct.engine import eval_batch  # noqa: E402
 from mpct.scenarios import SHELL7_TUNED, shell7x5, woodberry_toolbox  # noqa: E402
 from oracle.scenarios import shell7x5 as o_shell7x5, woodberry_toolbox as o_wb  # noqa: E402
-from oracle.toolbox_band import closedloop_band  # noqa: E402
+from oracle.toolbox_band import closedloop_band, replay_moves  # noqa: E402
 
 
 def cmp(name, sc, osc, r, v, cands, nit, open_loop=True):
@@ -23,6 +23,9 @@ def cmp(name, sc, osc, r, v, cands, nit, open_loop=True):
     t0 = time.time()
     res = eval_batch(sc, N2, Nu, D, Lm, r[None], v=v[None], open_loop=open_loop, want_traj=True, device=0)
     tg = time.time() - t0
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.savez(os.path.join(ROOT, "gpurun_out", "band_%s.npz" % name), N2=N2, Nu=Nu, D=D, L=Lm, u=res.u, y=res.y,
+             status=res.status, iters=res.qp_iters)
     worst = 0.0
     for k, c in enumerate(cands):
         t1 = time.time()
@@ -38,8 +41,14 @@ def cmp(name, sc, osc, r, v, cands, nit, open_loop=True):
             eu2 = np.abs(res.uopt[k] - o.uopt).max() / (np.abs(o.uopt).max() + 1e-30)
             msg += " ys %.2e uopt %.2e" % (ey2, eu2)
             worst = max(worst, ey2, eu2)
-        print(msg + "  (oracle %.2fs)" % to, flush=True)
-        worst = max(worst, ey, eu)
+        try:
+            du_o, du_a = replay_moves(osc, r, v, int(c[0]), int(c[1]), c[2], c[3], res.u[k])
+            erp = np.abs(du_o - du_a).max() / (np.abs(du_a).max() + 1e-30)
+        except Exception as e:  # noqa: BLE001
+            print("replay failed:", e)
+            erp = np.inf
+        print(msg + " replay %.2e  (oracle %.2fs)" % (erp, to), flush=True)
+        worst = max(worst, erp)
     print("%s: gpu %.3fs, worst rel %.3e" % (name, tg, worst), flush=True)
     return worst
 
