@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(64, 1)
   for (int i = 0; i < my; ++i) any_q = any_q || qw(i) > 0.0;
 
   const double tol = o.feas_tol;
-  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 10 * Mz + 64;
+  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 30 * Mz + 200;
   long long iters = 0;
   const double* rr = rv + (long long)kref * my * nit;
   const double* vvk = vv ? vv + (long long)kref * nd * nit : nullptr;
@@ -411,6 +411,73 @@ __global__ void __launch_bounds__(64, 1)
       wave_argmin64(best, bid);
     };
     int it = 0;
+    // exact solve of the equality problem on the active set from x_u (needs sxc = x_u and this
+    // lane's box slacks at x_u in s): J and R_A rebuilt from R^-1 when stale (or forced), then
+    // x = x_u + J_A w with R_A'w = b_A - N_A'x_u, dropping negative multipliers one at a time.
+    // Used for the warm start, and to re-centre long QPs whose incremental updates drift off the
+    // active rows (the N2 = 127 search range runs ~450 iterations in one QP).
+    auto eqp_from_xu = [&](const double s[4], bool force) __attribute__((always_inline)) -> double {
+      if (row) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
+      }
+      lds_sync();
+      if (force || !gis.jinit || gis.nrot >= 4 * Mz) {
+        const int qq = gis.q;
+        gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+        gis.q = 0;
+        for (int v = 0; v < qq; ++v) {
+          const int p = __builtin_amdgcn_readlane(gis.ww, v);
+          const double dk = dvec(p);
+          const double beta = qsum<MAXM>(lane >= v && row ? dk * dk : 0.0);
+          lds_sync();
+          const double zm = gi_z(sJT, sd, v, Mz, row);
+          const double uk = gis.uw;
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark);
+          if (lane == v) gis.uw = uk;
+          ++it;
+        }
+        gis.nrot = 0;
+      }
+      lds_sync();
+      double x = row ? xu : 0.0;
+      for (;;) {
+        const int q = gis.q;
+        if (q == 0) {
+          x = row ? xu : 0.0;
+          break;
+        }
+        double cc = 0.0;
+        if (lane < q) {
+          const int p = gis.ww;
+          cc = p < base ? -ssl[p] : -out_slack(F, p - base, sxc[M]);
+        }
+        double wv = 0.0;
+        x = row ? xu : 0.0;
+        for (int v = 0; v < q; ++v) {  // R_A'w = c, x = x_u + J(:,0:q) w
+          const double w = bcast(cc * gis.rdg, v);
+          if (lane == v) wv = w;
+          if (lane > v && lane < q) cc -= sRA[v * Mz + lane] * w;
+          if (row) x += sJT[v * Mz + lane] * w;
+        }
+        const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv);
+        if (lane < q) gis.uw = lam;
+        double lmin = lane < q ? lam : INFINITY;
+        int kd = lane;
+        qargmin<MAXM>(lmin, kd);
+        if (!(lmin < 0.0)) break;
+        gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark);
+        ++it;
+      }
+      return row ? x : 0.0;
+    };
+    // re-centre at x_u's slacks (recomputed: sxc and ssl hold the current iterate's)
+    auto recentre = [&](bool force) __attribute__((always_inline)) -> double {
+      double b0, s0[4];
+      int i0;
+      most_violated(row ? xu : 0.0, b0, i0, s0, true);
+      return eqp_from_xu(s0, force);
+    };
     double xm = row ? xu : 0.0;
     {
       double best, s[4];
@@ -424,71 +491,32 @@ __global__ void __launch_bounds__(64, 1)
       if (gis.q == 0) {
         gis.jinit = false;
       } else {
-        if (row) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
-        }
-        lds_sync();
-        if (!gis.jinit || gis.nrot >= 4 * Mz) {
-          // rebuild J (and R_A) for the retained set from R^-1
-          const int qq = gis.q;
-          gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
-          gis.q = 0;
-          for (int v = 0; v < qq; ++v) {
-            const int p = __builtin_amdgcn_readlane(gis.ww, v);
-            const double dk = dvec(p);
-            const double beta = qsum<MAXM>(lane >= v && row ? dk * dk : 0.0);
-            lds_sync();
-            const double zm = gi_z(sJT, sd, v, Mz, row);
-            const double uk = gis.uw;
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark);
-            if (lane == v) gis.uw = uk;
-            ++it;
-          }
-          gis.nrot = 0;
-        }
-        lds_sync();
-        // equality-constrained solve on the retained set from x_u, dropping negative multipliers
-        for (;;) {
-          const int q = gis.q;
-          if (q == 0) {
-            xm = row ? xu : 0.0;
-            break;
-          }
-          double cc = 0.0;
-          if (lane < q) {
-            const int p = gis.ww;
-            cc = p < base ? -ssl[p] : -out_slack(F, p - base, sxc[M]);
-          }
-          double wv = 0.0;
-          xm = row ? xu : 0.0;
-          for (int v = 0; v < q; ++v) {  // R_A'w = c, x = x_u + J(:,0:q) w
-            const double w = bcast(cc * gis.rdg, v);
-            if (lane == v) wv = w;
-            if (lane > v && lane < q) cc -= sRA[v * Mz + lane] * w;
-            if (row) xm += sJT[v * Mz + lane] * w;
-          }
-          const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv);
-          if (lane < q) gis.uw = lam;
-          double lmin = lane < q ? lam : INFINITY;
-          int kd = lane;
-          qargmin<MAXM>(lmin, kd);
-          if (!(lmin < 0.0)) break;
-          gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark);
-          ++it;
-        }
-        if (!row) xm = 0.0;
+        xm = eqp_from_xu(s, false);
       }
     }
+    int npolish = 0;
     for (;;) {
       double best, s[4];
       int bid;
       most_violated(xm, best, bid, s, false);
-      if (!(best < -tol)) break;
+      if (!(best < -tol)) {
+        // optimal up to the incremental updates: after a long QP re-solve the final active set
+        // exactly from x_u (fresh J) and re-check every row before accepting
+        if (gis.q > 0 && gis.nrot >= Mz && npolish < 2) {
+          ++npolish;
+          xm = recentre(true);
+          continue;
+        }
+        break;
+      }
       // a full active set (q == Mz) is legal here: beta = 0 forces dual steps (drops) first
       if (it >= maxit) {
         st |= MPCT_ST_QP_MAXITER_;
         break;
+      }
+      if (gis.q > 0 && gis.nrot >= 4 * Mz) {  // J has drifted: rebuild it and re-centre x
+        xm = recentre(true);
+        continue;
       }
       if (!gis.jinit) gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
       const int p = bid;
@@ -532,7 +560,11 @@ __global__ void __launch_bounds__(64, 1)
           break;
         }
       }
-      if (it >= maxit || infeas) break;
+      if (infeas) break;
+      if (it >= maxit) {
+        st |= MPCT_ST_QP_MAXITER_;
+        break;
+      }
     }
     if (row) sxc[lane] = xm;
     lds_sync();
@@ -697,6 +729,8 @@ __global__ void __launch_bounds__(64, 1)
     dbg_t = t;
     const int it_dbg = solve(Fc, r_t);
     iters += it_dbg;
+    if (sim == 0 && lane == 0 && t == MPCT_DEBUG_BAND - 3)
+      for (int m = 0; m < Mz; ++m) printf("X %d %.17e\n", m, sxc[m]);
     if (sim == 0 && lane == 0 && t < MPCT_DEBUG_BAND)
       printf("t=%d it=%d q=%d eps=%.9e du=%.9e %.9e %.9e F0=%.9e Fend=%.9e y6=%.9e st=%d\n", t, it_dbg, gis.q,
              sxc[M], sxc[0], sxc[Nu], sxc[2 * Nu], Fc[0], Fc[N2 - 1], Fc[6 * N2], st);

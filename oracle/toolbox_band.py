@@ -26,11 +26,12 @@ and ``MPCTuning.m:162-199`` configure:
   slack eps >= 0:  y_min_i - eps V^min_i s^y_i <= y_i(t+k|t) <= y_max_i + eps V^max_i s^y_i
   for every k = 1..p, with V = the MinECR/MaxECR of ``Shell7x5.m:143-152`` and s^y the OV
   ScaleFactor after ``MPCTuning.m:182-184``.
-* The QP is solved to optimality by the primal active-set method of ``toolbox_gpc.py``
-  (Nocedal & Wright Alg. 16.3, null-space steps by lstsq) started from the feasible point
-  (dU = 0, eps = the smallest slack that satisfies every soft row).  The device uses a dual
-  (Goldfarb-Idnani) method.  The QP is strictly convex (lambda > 0, rho > 0), so both reach
-  the same minimiser.
+* The QP (strictly convex: lambda > 0, rho > 0) is equilibrated (unit Hessian diagonal, unit
+  constraint rows: rho*eps outweighs lambda^2*du by ~9 orders of magnitude on Shell 7x5) and
+  solved by a dense textbook dual active-set method (``qp_dual_dense``: everything recomputed
+  each iteration, no updates, no warm start).  A primal active-set method cycles on the
+  ~1.8k near-parallel output rows of the N2 = 127 search range.  Every solution must pass an
+  algorithm-independent KKT check (``kkt_residual``: NNLS multipliers on the active rows).
 * Open-loop first-move prediction (``closedloop_toolbox.m:85-100``): the QP at the initial
   state with reference r(:,end) and MD v(:,end) held from time 0 gives Info.Uopt, padded to
   nit.  Then ys = lsim(Pz, [uopt v]) with the actual v.
@@ -166,6 +167,93 @@ def qp_primal_active_set_x0(W, c, Ain, bin_, x0, tol=1e-12, maxit=2000):
     raise RuntimeError("primal active set did not converge")
 
 
+def qp_dual_dense(W, c, A, b, tol=1e-12, maxit=5000):
+    """min 1/2 ||W x + c||^2 s.t. A x >= b by the textbook dual method of Goldfarb & Idnani
+    (1983), recomputed densely at every iteration: in the coordinates w = L'x (H = W'W = LL')
+    the Hessian is I, the primal direction is the projection of n_p onto null(N_A) and the dual
+    direction solves N_A' r = n_p, both from a fresh QR of the active rows (never N H^-1 N',
+    which squares their conditioning at the near-dependent vertices of the output bands); after
+    every addition the iterate is re-solved exactly on the active set.  No factor updates and no
+    warm start: the device's J-form / Householder / warm-started variant shares none of this
+    arithmetic.  The dual objective increases monotonically, so the ~1.8k near-parallel output
+    rows of the N2 = 127 range cannot make it cycle.  Returns (x, iterations, active set)."""
+    import scipy.linalg as sla
+
+    H = W.T @ W
+    g = W.T @ c
+    L = np.linalg.cholesky(H)
+    Aw = sla.solve_triangular(L, A.T, lower=True).T          # rows of A L^-T
+    gw = sla.solve_triangular(L, g, lower=True)
+    w = -gw
+    act, u = [], np.zeros(0)
+    it = 0
+
+    def factor():
+        Q, R = np.linalg.qr(Aw[act].T, mode="complete")
+        q = len(act)
+        return Q[:, :q], Q[:, q:], R[:q, :q]
+
+    while True:
+        s = Aw @ w - b
+        if act:
+            s[act] = np.inf
+        p = int(np.argmin(s))
+        if not s[p] < -tol * max(1.0, abs(b[p])):
+            return sla.solve_triangular(L.T, w, lower=False), it, act
+        n = Aw[p]
+        up = np.concatenate([u, [0.0]])
+        while True:
+            it += 1
+            if it > maxit:
+                raise RuntimeError("dual active set did not converge")
+            if act:
+                Q1, Q2, R = factor()
+                z = Q2 @ (Q2.T @ n)
+                r = sla.solve_triangular(R, Q1.T @ n, lower=False)
+            else:
+                z, r = n.copy(), np.zeros(0)
+            zn = float(z @ n)
+            t2 = -(float(n @ w) - b[p]) / zn if zn > 1e-14 * float(n @ n) else np.inf
+            pos = np.nonzero(r > 0)[0]
+            t1, k = np.inf, -1
+            if pos.size:
+                ratios = up[pos] / r[pos]
+                j = int(np.argmin(ratios))
+                t1, k = float(ratios[j]), int(pos[j])
+            t = min(t1, t2)
+            if not np.isfinite(t):
+                raise RuntimeError("QP infeasible")
+            if np.isfinite(t2):
+                w = w + t * z
+            up[:-1] -= t * r
+            up[-1] += t
+            if t2 <= t1:
+                act.append(p)
+                # exact re-solve on the active set: w = -gw + Q1 R^-T (b_A + N_A gw)
+                Q1, _, R = factor()
+                y = sla.solve_triangular(R, b[act] + Aw[act] @ gw, lower=False, trans="T")
+                w = -gw + Q1 @ y
+                u = np.maximum(sla.solve_triangular(R, y, lower=False), 0.0)
+                break
+            del act[k]
+            up = np.delete(up, k)
+
+
+def kkt_residual(W, c, A, b, x, tol=1e-9):
+    """Algorithm-independent optimality measure of x: NNLS multipliers on the rows active at x,
+    relative stationarity residual (0 at a KKT point) and the most negative slack."""
+    from scipy.optimize import nnls
+
+    grad = W.T @ (W @ x + c)
+    s = A @ x - b
+    act = np.abs(s) <= tol * np.maximum(1.0, np.abs(b))
+    gn = max(1.0, float(np.linalg.norm(grad)))
+    if not act.any():
+        return float(np.linalg.norm(grad)) / gn, float(s.min(initial=np.inf))
+    _, rn = nnls(A[act].T, grad)
+    return rn / gn, float(s.min())
+
+
 def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     """One toolbox QP: returns (x = [dU; eps], iterations).  f: free response (my*N2),
     q: per-output tracking weight, wl: per-MV move weight (already squared / scaled)."""
@@ -220,7 +308,11 @@ def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     As = A * dsc[None, :]
     rn = np.linalg.norm(As, axis=1)
     rn[rn == 0] = 1.0
-    y, it, _ = qp_primal_active_set_x0(W * dsc[None, :], c, As / rn[:, None], b / rn, x0 / dsc)
+    Ws, As, bs = W * dsc[None, :], As / rn[:, None], b / rn
+    y, it, _ = qp_dual_dense(Ws, c, As, bs)
+    res, smin = kkt_residual(Ws, c, As, bs, y)
+    if res > 1e-8 or smin < -1e-9:
+        raise RuntimeError("oracle QP failed its KKT check (residual %.2e, slack %.2e)" % (res, smin))
     return y * dsc, it
 
 

@@ -1,0 +1,241 @@
+"""Measured-disturbance feed-forward + soft output bands (config 3 Shell7x5.m; WoodBerry.m's
+toolbox MPC).  CPU: the oracle restatement (oracle/toolbox_band.py) is pinned to the reference's
+committed Shell 7x5 tuning file (plant, bounds, ECR, ScaleFactors, Weights.ECR) and to the
+identities of the toolbox prediction and QP: the one-step prediction equals the next measured
+output (nominal loop), and every QP solution satisfies KKT (NNLS multipliers, equilibrated).
+GPU (-m gpu): the mdband kernel through the C ABI against that oracle -- free-run trajectories
+for stable closed loops, and a per-step replay (the oracle's QP optimum at the state the device
+actually reached) for every candidate, since switching / unstable band loops amplify rounding.
+Trajectories and costs against MATLAB's MPC Toolbox itself: parity unpinned (closed source, no
+committed trajectories)."""
+import numpy as np
+import pytest
+
+TRAJ_RTOL = 1e-7      # free-run trajectories, relative to the trajectory's peak
+REPLAY_RTOL = 1e-6    # per-step first moves at the device's own states, relative to max |du|
+COST_RTOL = 1e-6      # BASELINE tolerance on the costs
+
+
+def _trel(a, b):
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-300))
+
+
+def test_shell7x5_oracle_scenario_pinned_to_fixture():
+    """Shell7x5_Tuning_14Sep2024_14_22.mat (decoded fixture): the scaled discrete [Gs Ds] of
+    c2d + L, R, the OV bounds/ECR/ScaleFactors and MV bounds equal the saved mpc object's."""
+    from oracle.scenarios import shell7x5
+
+    sc, r, v, yref, fx = shell7x5()
+    ps = fx["plant_scaled_discrete"]
+    num, den, dl = np.array(ps["num"]), np.array(ps["den"]), np.array(ps["iodelay"])
+    for i in range(7):
+        for j in range(5):
+            e = sc.plant[i][j]
+            np.testing.assert_allclose(e.num, num[i, j], rtol=0, atol=1e-14)
+            np.testing.assert_allclose(e.den, den[i, j], rtol=0, atol=1e-14)
+            assert e.iodelay == dl[i, j]
+    ov, mv = fx["OV"], fx["MV"]
+    np.testing.assert_allclose(sc.y_max, [o["Max"] for o in ov], rtol=1e-15)
+    np.testing.assert_allclose(sc.y_min, [o["Min"] for o in ov], rtol=1e-15)
+    np.testing.assert_allclose(sc.ecr_max, [o["MaxECR"] for o in ov])
+    np.testing.assert_allclose(sc.sy, [o["ScaleFactor"] for o in ov], rtol=1e-15)
+    np.testing.assert_allclose(sc.u_max, [m["Max"] for m in mv], rtol=1e-15)
+    np.testing.assert_allclose(sc.su, [m["ScaleFactor"] for m in mv])
+    assert all(m["RateMax"] == "inf" for m in mv)
+    assert fx["Weights"]["ECR"] == [sc.rho] and fx["Weights"]["OutputVariables"] == [0.0] * 7
+
+
+def test_product_shell7x5_signals_match_oracle():
+    from mpct.scenarios import SHELL7_L, SHELL7_R, shell7x5_plant, shell7x5_signals
+    from oracle.scenarios import shell7x5
+
+    osc, r, v, yref, fx = shell7x5()
+    np.testing.assert_allclose(SHELL7_L, fx["scale"]["L"], rtol=0)
+    np.testing.assert_allclose(SHELL7_R, fx["scale"]["R"], rtol=0)
+    pr, pv, py = shell7x5_signals()
+    np.testing.assert_array_equal(pr, r)
+    np.testing.assert_allclose(pv, v, rtol=1e-15)
+    np.testing.assert_allclose(py, yref, rtol=1e-12, atol=1e-15)
+    P = shell7x5_plant()
+    for i in range(7):
+        for j in range(5):
+            np.testing.assert_allclose(P[i][j].num, osc.plant[i][j].num, rtol=1e-13, atol=1e-16)
+
+
+def test_band_oracle_identities():
+    """Nominal toolbox loop: (1) the one-step prediction y(t+1|t) = F_t[0] + sum_n s_n(1) du_n(t)
+    equals the next measured output; (2) every QP solution is a KKT point of the equilibrated
+    problem (NNLS multipliers on the active rows)."""
+    from scipy.optimize import nnls
+
+    import oracle.toolbox_band as tb
+    from oracle.scenarios import shell7x5
+    from oracle.toolbox_gpc import constraint_rows
+
+    sc, r, v, yref, fx = shell7x5(nit=60)
+    N2, Nu = 12, 3
+    lam = np.array(fx["lambda"])
+    calls = []
+    orig = tb.band_qp
+
+    def spy(sc_, G, f, rvec, u_prev, N2_, Nu_, q, wl):
+        x, it = orig(sc_, G, f, rvec, u_prev, N2_, Nu_, q, wl)
+        calls.append((G, f, u_prev, wl, x))
+        return x, it
+
+    tb.band_qp = spy
+    try:
+        tr = []
+        res = tb.closedloop_band(sc, r, v, N2, Nu, np.zeros(7), lam, 60, open_loop=False, trace=tr)
+    finally:
+        tb.band_qp = orig
+    S = tb.step_table(sc, N2 + 2)
+    for t in range(59):
+        pred = tr[t][0::N2] + S[:, :3, 1] @ res.du_hist[:, t]
+        np.testing.assert_allclose(pred, res.y[:, t + 1], rtol=1e-10, atol=1e-13)
+    M = 3 * Nu
+    for G, f, up, wl, x in calls[18:40]:
+        Ab, bb = constraint_rows(3, Nu, sc.du_min, sc.du_max, sc.u_min, sc.u_max, up)
+        A = [np.hstack([Ab, np.zeros((Ab.shape[0], 1))]), np.eye(1, M + 1, M)]
+        b = [bb, np.zeros(1)]
+        for i in range(7):
+            Gi, fi = G[i * N2:(i + 1) * N2], f[i * N2:(i + 1) * N2]
+            A += [np.hstack([-Gi, np.full((N2, 1), sc.ecr_max[i] * sc.sy[i])]),
+                  np.hstack([Gi, np.full((N2, 1), sc.ecr_min[i] * sc.sy[i])])]
+            b += [fi - sc.y_max[i], sc.y_min[i] - fi]
+        A, b = np.vstack(A), np.concatenate(b)
+        h = np.concatenate([np.repeat(wl, Nu), [sc.rho]])
+        s = A @ x - b
+        assert s.min() > -1e-12 * max(1.0, np.abs(b).max())
+        act = np.abs(s) <= 1e-9 * np.maximum(1.0, np.abs(b))
+        d = 1.0 / np.sqrt(h)
+        grad = h * x * d
+        if not act.any():
+            assert np.linalg.norm(grad) < 1e-10
+            continue
+        _, rn = nnls((A[act] * d).T, grad)
+        assert rn <= 1e-9 * max(1.0, np.linalg.norm(grad)), rn
+
+
+@pytest.fixture(scope="module")
+def gpu(built, has_gpu):
+    if not has_gpu:
+        pytest.skip("no GPU")
+    return True
+
+
+def _shell_cands():
+    """The config-3 tuned point plus seeded candidates across the band search space (delta = 0),
+    two with tracking weights on outputs 3..7 (the general H = R'R path)."""
+    from mpct.scenarios import SHELL7_TUNED
+
+    rng = np.random.default_rng(7)
+    c = [(27, 2, np.zeros(7), np.array(SHELL7_TUNED["lam"]))]
+    for _ in range(5):
+        c.append((int(rng.integers(5, 41)), int(rng.integers(1, 9)), np.zeros(7), 10 ** rng.uniform(-3, 1, 3)))
+    for _ in range(2):
+        d = np.concatenate([np.zeros(2), 10 ** rng.uniform(-2, 0, 5)])
+        c.append((int(rng.integers(5, 41)), int(rng.integers(1, 9)), d, 10 ** rng.uniform(-3, 1, 3)))
+    return [x for x in c if x[1] <= x[0]]
+
+
+def _run(sc, cands, r, v, open_loop=True):
+    from mpct.engine import eval_batch
+
+    N2 = np.array([c[0] for c in cands], np.int32)
+    Nu = np.array([c[1] for c in cands], np.int32)
+    return eval_batch(sc, N2, Nu, np.array([c[2] for c in cands]), np.array([c[3] for c in cands]),
+                      r[None], v=v[None], open_loop=open_loop, want_traj=True)
+
+
+@pytest.mark.gpu
+def test_band_shell7x5_tuned_point(gpu):
+    """Shell 7x5 at the committed tuning (N = 27, Nu = 2, delta = 0, lambda of the .mat):
+    trajectories, open-loop prediction and all cost terms against the oracle."""
+    from mpct.scenarios import SHELL7_TUNED, shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import closedloop_band
+
+    sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    lam = np.array(SHELL7_TUNED["lam"])
+    res = _run(sc, [(27, 2, np.zeros(7), lam)], r, v)
+    ref = closedloop_band(osc, orr, ov, 27, 2, np.zeros(7), lam, 200)
+    assert res.status[0] == 0
+    for a, b in ((res.y[0], ref.y), (res.u[0], ref.u), (res.ys[0], ref.ys), (res.uopt[0], ref.uopt)):
+        assert _trel(a, b) < TRAJ_RTOL, _trel(a, b)
+    ink = 9
+    np.testing.assert_allclose(res.J1[0], ((ref.y - oyref) ** 2).sum(1), rtol=COST_RTOL)
+    np.testing.assert_allclose(res.j22[0], ((ref.y - oyref)[:, ink:] ** 2).sum(1), rtol=COST_RTOL)
+    np.testing.assert_allclose(res.j21[0], ((ref.y - ref.ys)[:, ink:] ** 2).sum(1), rtol=COST_RTOL)
+
+
+@pytest.mark.gpu
+def test_band_shell7x5_replay(gpu):
+    """Every seeded candidate takes the oracle's optimal move at every step of its own closed
+    loop; the open-loop prediction (one QP from rest) matches directly."""
+    from mpct.scenarios import shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import closedloop_band, replay_moves
+
+    sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    cands = _shell_cands()
+    res = _run(sc, cands, r, v)
+    assert np.all(res.status == 0), res.status
+    for k, c in enumerate(cands):
+        du_o, du_a = replay_moves(osc, orr, ov, c[0], c[1], c[2], c[3], res.u[k])
+        assert _trel(du_a, du_o) < REPLAY_RTOL, (k, _trel(du_a, du_o))
+        ref = closedloop_band(osc, orr, ov, c[0], c[1], c[2], c[3], 200)
+        assert _trel(res.uopt[k], ref.uopt) < TRAJ_RTOL and _trel(res.ys[k], ref.ys) < TRAJ_RTOL, k
+
+
+@pytest.mark.gpu
+def test_band_woodberry_toolbox(gpu):
+    """WoodBerry.m's toolbox MPC (one measured disturbance, rate + amplitude bounds, tracking
+    weights, no output bands): trajectories and costs against the oracle."""
+    from mpct.scenarios import woodberry_toolbox
+    from oracle.scenarios import woodberry_toolbox as o_wb
+    from oracle.toolbox_band import closedloop_band
+
+    sc, r, v, yref = woodberry_toolbox()
+    osc, orr, ov, oyref = o_wb()
+    rng = np.random.default_rng(11)
+    cands = [(int(rng.integers(5, 31)), int(rng.integers(1, 11)), 10 ** rng.uniform(-2, 0, 2),
+              10 ** rng.uniform(-3, 0, 2)) for _ in range(4)]
+    cands = [c for c in cands if c[1] <= c[0]]
+    res = _run(sc, cands, r, v)
+    assert np.all(res.status == 0)
+    for k, c in enumerate(cands):
+        ref = closedloop_band(osc, orr, ov, c[0], c[1], c[2], c[3], 400)
+        assert _trel(res.y[k], ref.y) < TRAJ_RTOL and _trel(res.u[k], ref.u) < TRAJ_RTOL, k
+        np.testing.assert_allclose(res.J1[k], ((ref.y - oyref) ** 2).sum(1), rtol=COST_RTOL)
+
+
+@pytest.mark.gpu
+def test_band_search_range_horizon(gpu):
+    """The largest VNS horizon of config 3 (N2 = 127, Nu = 15: 46 QP rows, the MAXM = 64 kernel,
+    2*7*127 output rows): per-step replay over the disturbance transient."""
+    from mpct.scenarios import shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import replay_moves
+
+    sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    lam = np.array([0.05, 0.02, 1.6])
+    res = _run(sc, [(127, 15, np.zeros(7), lam)], r, v, open_loop=False)
+    assert res.status[0] == 0
+    du_o, du_a = replay_moves(osc, orr, ov, 127, 15, np.zeros(7), lam, res.u[0], T=45)
+    assert _trel(du_a, du_o) < REPLAY_RTOL, _trel(du_a, du_o)
+
+
+@pytest.mark.gpu
+def test_band_deterministic_and_order_free(gpu):
+    from mpct.scenarios import shell7x5
+
+    sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+    cands = _shell_cands()
+    a = _run(sc, cands, r, v)
+    b = _run(sc, cands[::-1], r, v)
+    np.testing.assert_array_equal(a.J1, b.J1[::-1])
+    np.testing.assert_array_equal(a.u, b.u[::-1])

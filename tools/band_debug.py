@@ -50,7 +50,7 @@ def gpu():
         sc, r, v, yref = woodberry_toolbox()
         D = np.array([float(x) for x in DEL.split(",")])[None]
     else:
-        sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+        sc, r, v, yref = shell7x5(n2_max=int(os.environ.get("N2MAX", "40")), nu_max=int(os.environ.get("NUMAX", "8")))
         D = np.zeros((1, 7))
     res = eval_batch(sc, [N2], [NU], D, LAM[None], r[None], v=v[None], open_loop=False, device=0)
     torch.cuda.synchronize()
