@@ -37,6 +37,9 @@ struct BandLayout {
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
+// LDS copy of the MV step table: samples 0..N2 (+1 spare) of each entry, row stride tls
+__host__ __device__ inline int band_tls(const DevScenario& sc, int N2) { return sc.tlen < N2 + 2 ? sc.tlen : N2 + 2; }
+
 __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2, int M) {
   const int Mz = M + 1, my = sc.my, nu = sc.nu, nin = sc.nin, ne = sc.ne;
   BandLayout L;
@@ -65,7 +68,7 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.pla = take(ne * sc.pl_maxa);
   L.mzb = take(ne * sc.mz_maxb);
   L.mza = take(ne * sc.mz_maxa);
-  L.step = take(my * nu * sc.tlen);
+  L.step = take(my * nu * band_tls(sc, N2));
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -91,7 +94,8 @@ __global__ void __launch_bounds__(64, 1)
     mdband_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
                               const int* __restrict__ Nuv, const double* __restrict__ deltav,
                               const double* __restrict__ lambdav, const double* __restrict__ rv,
-                              const double* __restrict__ vv, const DevOpts o, const DevResult out) {
+                              const double* __restrict__ vv, const DevOpts o, const DevResult out,
+                              int mz_lo, long long lds_lo, long long lds_hi, int first) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const long long sim = blockIdx.x;
@@ -117,14 +121,17 @@ __global__ void __launch_bounds__(64, 1)
     }
   };
   if (N2 <= 0) {
-    write_nan(MPCT_ST_SKIPPED_);
+    if (first) write_nan(MPCT_ST_SKIPPED_);
     return;
   }
-  if (N2 > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N2 || Mz > MAXM) {
-    write_nan(MPCT_ST_BADHORIZON_);
+  if (N2 > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N2) {
+    if (first) write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
   const BandLayout L = band_layout(sc, N2, M);
+  // this launch serves one (QP size, LDS) class: the others' simulations leave at once
+  if (Mz <= mz_lo || Mz > MAXM || (long long)L.total * 8 <= lds_lo || (long long)L.total * 8 > lds_hi) return;
+  const int tls = band_tls(sc, N2);
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
@@ -151,7 +158,10 @@ __global__ void __launch_bounds__(64, 1)
   double* sstep = lds + L.step;
 
   // ------------------------------------------------------------------ prologue
-  for (int e = lane; e < my * nu * tlen; e += kWave) sstep[e] = sc.step[e];
+  for (int e = lane; e < my * nu * tls; e += kWave) {
+    const int en = e / tls;
+    sstep[e] = sc.step[en * tlen + (e - en * tls)];
+  }
   for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
   for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
   for (int e = lane; e < ne * sc.mz_maxb; e += kWave) smzb[e] = sc.mz_b[e];
@@ -198,7 +208,7 @@ __global__ void __launch_bounds__(64, 1)
         double w = 0.0;
         if (lane < M) {
           const int tt = 1 + r - rcn.l;
-          w = tt >= 0 ? sq * sstep[(i * nu + rcn.n) * tlen + tt] : 0.0;
+          w = tt >= 0 ? sq * sstep[(i * nu + rcn.n) * tls + tt] : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < MAXM; ++k) {
@@ -244,7 +254,7 @@ __global__ void __launch_bounds__(64, 1)
   for (int i = 0; i < my; ++i) any_q = any_q || qw(i) > 0.0;
 
   const double tol = o.feas_tol;
-  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 30 * Mz + 200;
+  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 200 * Mz + 1000;
   long long iters = 0;
   const double* rr = rv + (long long)kref * my * nit;
   const double* vvk = vv ? vv + (long long)kref * nd * nit : nullptr;
@@ -262,7 +272,7 @@ __global__ void __launch_bounds__(64, 1)
     double a0 = F[g], a1 = 0.0;
     const int lmax = min(Nu - 1, k + 1);
     for (int n = 0; n < nu; ++n) {
-      const double* sp = sstep + (i * nu + n) * tlen + (k + 1);
+      const double* sp = sstep + (i * nu + n) * tls + (k + 1);
       const double* xp = sxc + n * Nu;
       int l = 0;
       for (; l + 1 <= lmax; l += 2) {
@@ -298,7 +308,7 @@ __global__ void __launch_bounds__(64, 1)
         const int q = p - base, g = q >> 1, i = g / N2, k = g - i * N2;
         if (lane < M) {
           const int tt = k + 1 - rcn.l;
-          nvv = tt >= 0 ? sstep[(i * nu + rcn.n) * tlen + tt] : 0.0;
+          nvv = tt >= 0 ? sstep[(i * nu + rcn.n) * tls + tt] : 0.0;
           if (!(q & 1)) nvv = -nvv;
         } else {
           nvv = sob[((q & 1) ? 2 : 3) * my + i];
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(64, 1)
           const double qi = qw(i);
           if (!(qi > 0.0)) continue;
           const double ri = sgv[i];
-          const double* sp = sstep + (i * nu + rcn.n) * tlen;
+          const double* sp = sstep + (i * nu + rcn.n) * tls;
           for (int k = rcn.l > 0 ? rcn.l - 1 : 0; k < N2; ++k) g += qi * sp[k + 1 - rcn.l] * (F[i * N2 + k] - ri);
         }
       }
@@ -410,7 +420,8 @@ __global__ void __launch_bounds__(64, 1)
       }
       wave_argmin64(best, bid);
     };
-    int it = 0;
+    int it = 0;   // all factorisation work (GI steps + rebuild re-adds + re-centring drops): qp_iters
+    int git = 0;  // GI add/drop steps only: the iteration cap guards against cycling, not rebuilds
     // exact solve of the equality problem on the active set from x_u (needs sxc = x_u and this
     // lane's box slacks at x_u in s): J and R_A rebuilt from R^-1 when stale (or forced), then
     // x = x_u + J_A w with R_A'w = b_A - N_A'x_u, dropping negative multipliers one at a time.
@@ -510,7 +521,7 @@ __global__ void __launch_bounds__(64, 1)
         break;
       }
       // a full active set (q == Mz) is legal here: beta = 0 forces dual steps (drops) first
-      if (it >= maxit) {
+      if (git >= maxit) {
         st |= MPCT_ST_QP_MAXITER_;
         break;
       }
@@ -524,6 +535,7 @@ __global__ void __launch_bounds__(64, 1)
       bool infeas = false;
       for (;;) {
         ++it;
+        ++git;
         const double dk = dvec(p);
         const double d2 = row ? dk * dk : 0.0;
         const double dn2 = qsum<MAXM>(d2);
@@ -538,7 +550,7 @@ __global__ void __launch_bounds__(64, 1)
           kdrop = lane;
         }
         qargmin<MAXM>(t1, kdrop);
-        const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
+        const double t2 = (beta > 1e-20 * dn2) ? -sp / beta : INFINITY;
         if (t1 == INFINITY && t2 == INFINITY) {
           st |= MPCT_ST_QP_INFEAS_;
           infeas = true;
@@ -555,13 +567,13 @@ __global__ void __launch_bounds__(64, 1)
           break;
         }
         gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark);
-        if (it >= maxit) {
+        if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;
           break;
         }
       }
       if (infeas) break;
-      if (it >= maxit) {
+      if (git >= maxit) {
         st |= MPCT_ST_QP_MAXITER_;
         break;
       }
@@ -672,7 +684,7 @@ __global__ void __launch_bounds__(64, 1)
       if (j < nu) {
         const double dlt = sdu[j];
         if (dlt != 0.0) {
-          const double* sp = sstep + (i * nu + j) * tlen;
+          const double* sp = sstep + (i * nu + j) * tls;
           for (int l = 0; l < na; ++l)
             if (N2 - l >= 0) tl[l] += sp[N2 - l] * dlt;
         }
@@ -710,7 +722,7 @@ __global__ void __launch_bounds__(64, 1)
       double f;
       if (k < N2 - 1) {
         f = Fp[g + 1];
-        for (int n = 0; n < nu; ++n) f += sstep[(i * nu + n) * tlen + k + 2] * sdu[n];
+        for (int n = 0; n < nu; ++n) f += sstep[(i * nu + n) * tls + k + 2] * sdu[n];
         if (any_dv) {
           for (int m = 0; m < nd; ++m) {
             const double* vr = sur + (nu + m) * kURing;
@@ -777,6 +789,7 @@ __global__ void __launch_bounds__(64, 1)
 
 // ------------------------------------------------------------------------------------------
 // host-side launch
+#include <algorithm>
 #include <string>
 
 namespace mpct {
@@ -786,29 +799,45 @@ long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu) {
   return (long long)L.total * 8;
 }
 
+// One launch per (QP size class MAXM, occupancy class): the dynamic LDS of a launch is what its
+// class's largest simulation needs, so short-horizon candidates are not held to the occupancy of
+// the scenario's (n2_max, nu_max) corner (one workgroup per CU at Shell 7x5's 104 KiB).  Every
+// launch spans the whole batch; a simulation runs in the one launch whose class holds its
+// (Mz, LDS bytes) and leaves the others at once (no host round trip to bucket device-resident
+// candidates).  Status-only outcomes (padding, bad horizons) are written by the first launch.
 template <int MAXM>
 static int launch_band_t(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                          const double* delta, const double* lambda, const double* r, const double* v,
-                         const DevOpts& o, const DevResult& out, hipStream_t stream, std::string* err) {
-  const long long lds = mdband_lds_bytes(sc, sc.n2max, sc.numax);
-  if (lds > 160 * 1024) {
+                         const DevOpts& o, const DevResult& out, hipStream_t stream, int mz_lo, bool& first,
+                         std::string* err) {
+  const int nu_hi = std::min(sc.numax, (MAXM - 1) / sc.nu);
+  if (nu_hi < 1) return 0;
+  const long long lds_max = mdband_lds_bytes(sc, sc.n2max, nu_hi);
+  if (lds_max > 160 * 1024) {
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
   auto kern = mdband_closed_loop_kernel<MAXM>;
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess) {
-      *err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed";
+  static const long long caps[4] = {40 * 1024, 53 * 1024, 80 * 1024, 160 * 1024};  // 4/3/2/1 per CU
+  long long lo = 0;
+  for (int k = 0; k < 4 && lo < lds_max; ++k) {
+    const long long lds = std::min(caps[k], lds_max);
+    if (lds > 64 * 1024) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds) != hipSuccess) {
+        *err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed";
+        return -3;
+      }
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
+                       delta, lambda, r, v, o, out, mz_lo, lo, lds, first ? 1 : 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
       return -3;
     }
-  }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
-                     delta, lambda, r, v, o, out);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
-    return -3;
+    first = false;
+    lo = lds;
   }
   return 0;
 }
@@ -817,11 +846,15 @@ int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, c
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
                   hipStream_t stream, std::string* err) {
   const int Mz = sc.nu * sc.numax + 1;
-  if (Mz <= 16) return launch_band_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
-  if (Mz <= 32) return launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
-  if (Mz <= 64) return launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, err);
-  *err = "nu*nu_max + 1 > 64";
-  return -4;
+  if (Mz > 64) {
+    *err = "nu*nu_max + 1 > 64";
+    return -4;
+  }
+  bool first = true;
+  int rc = launch_band_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 0, first, err);
+  if (rc == 0 && Mz > 16) rc = launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 16, first, err);
+  if (rc == 0 && Mz > 32) rc = launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 32, first, err);
+  return rc;
 }
 
 }  // namespace mpct

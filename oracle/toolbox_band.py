@@ -213,7 +213,7 @@ def qp_dual_dense(W, c, A, b, tol=1e-12, maxit=5000):
             else:
                 z, r = n.copy(), np.zeros(0)
             zn = float(z @ n)
-            t2 = -(float(n @ w) - b[p]) / zn if zn > 1e-14 * float(n @ n) else np.inf
+            t2 = -(float(n @ w) - b[p]) / zn if zn > 1e-20 * float(n @ n) else np.inf
             pos = np.nonzero(r > 0)[0]
             t1, k = np.inf, -1
             if pos.size:

@@ -239,3 +239,52 @@ def test_band_deterministic_and_order_free(gpu):
     b = _run(sc, cands[::-1], r, v)
     np.testing.assert_array_equal(a.J1, b.J1[::-1])
     np.testing.assert_array_equal(a.u, b.u[::-1])
+
+
+def test_band_oracle_near_dependent_rows():
+    """A QP captured from the config-3 grid (candidate 17703: N2 = 32, Nu = 3, the step the
+    measured disturbance enters; equilibrated rows): the vertex optimum needs a step along a
+    primal direction |z| ~ 1e-8 |n| between near-parallel output rows.  A dependence test at
+    |z|^2 <= 1e-14 |n|^2 calls this feasible QP (an LP finds a point) infeasible; the dual method
+    must take the step and land on a KKT point."""
+    import oracle.toolbox_band as tb
+    from scipy.optimize import linprog
+
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                           "band_qp_near_dependent.npz"))
+    W, c, A, b = d["W"], d["c"], d["A"], d["b"]
+    n = A.shape[1]
+    lp = linprog(np.r_[np.zeros(n - 1), 1.0], A_ub=-A, b_ub=-b, bounds=[(None, None)] * n, method="highs")
+    assert lp.status == 0
+    x, it, act = tb.qp_dual_dense(W, c, A, b)
+    res, smin = tb.kkt_residual(W, c, A, b, x)
+    assert res < 1e-8 and smin > -1e-9, (res, smin)
+
+
+@pytest.mark.gpu
+def test_band_config3_grid_hard_cases(gpu):
+    """Config-3 grid candidates that once failed on the device (a near-dependent add declared
+    infeasible; ~500-iteration cold QPs at the disturbance step over the cap): status 0, the
+    oracle's optimal move at every step of the transient, and the same bits whether scored alone
+    or in one mixed batch (each (QP size, LDS) class runs in its own launch)."""
+    import sys
+
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "..", "tools"))
+    from bench_config3 import grid
+    from mpct.scenarios import shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import replay_moves
+
+    sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    N2, Nu, D, L = grid(1024)
+    idx = [5485, 17703, 29829]
+    cands = [(int(N2[k]), int(Nu[k]), D[k], L[k]) for k in idx]
+    res = _run(sc, cands, r, v, open_loop=False)
+    assert np.all(res.status == 0), res.status
+    for k, c in enumerate(cands):
+        du_o, du_a = replay_moves(osc, orr, ov, c[0], c[1], c[2], c[3], res.u[k], T=40)
+        assert _trel(du_a, du_o) < REPLAY_RTOL, (idx[k], _trel(du_a, du_o))
+        one = _run(sc, [c], r, v, open_loop=False)
+        np.testing.assert_array_equal(one.u[0], res.u[k])
+        np.testing.assert_array_equal(one.J1[0], res.J1[k])

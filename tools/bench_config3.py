@@ -75,6 +75,7 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rec, f, indent=1)
+        np.savez_compressed(os.path.splitext(a.out)[0] + ".npz", status=st, qp_iters=it, J1=J1)
 
 
 if __name__ == "__main__":
