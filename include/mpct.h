@@ -29,8 +29,9 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 3 /* 3: MD feed-forward + soft output bands; 2: DTC-GPC predictor + plant-only
-                              disturbances + plant variants; v1 and v2 descriptors accepted */
+#define MPCT_ABI_VERSION 4 /* 4: nonlinear MPC scenarios (mpct_nmpc_scenario_create); 3: MD feed-forward +
+                              soft output bands; 2: DTC-GPC predictor + plant-only disturbances + plant
+                              variants; v1..v3 descriptors accepted */
 
 /* error codes */
 #define MPCT_OK 0
@@ -46,6 +47,8 @@ extern "C" {
 #define MPCT_ST_NONFINITE 4    /* a non-finite value appeared in the state           */
 #define MPCT_ST_SKIPPED 8      /* padding / sentinel candidate (N2 <= 0)             */
 #define MPCT_ST_BADHORIZON 16  /* N2/Nu outside the scenario's range or Nu > N2      */
+#define MPCT_ST_SQP_MAXITER 32 /* NMPC: a Gauss-Newton SQP hit sqp_max at some step  */
+#define MPCT_ST_BOUNDS 64      /* NMPC: the closed loop left the state/OV bounds     */
 
 /* One SISO discrete transfer function  y = z^-delay * num(z)/den(z) u  in the form tfdata(.,'v')
  * returns it (descending powers of z, numerator padded to the denominator's length, den[0]=1)
@@ -139,6 +142,57 @@ typedef struct mpct_scenario_desc {
 } mpct_scenario_desc;
 
 typedef struct mpct_scenario mpct_scenario;
+
+/* Nonlinear MPC scenario (config 5): the seam
+ *   function [y,u,yopt,uopt] = closedloop_toolbox_nmpc(nmpcobj,model,init,r,N,Nu,delta,lambda,nit)
+ *   (Matlab-Toolbox/NMPC/closedloop_toolbox_nmpc.m:1; callers VNS2.m:155, GAM_fun.m:87,
+ *   MPC-Tuning/VanDeVusse_NMPC.m:244).  MATLAB passes the model as a function handle; a C ABI
+ *   cannot carry one to the GPU, so the model is chosen from the library's built-in families by id
+ *   with its parameters:
+ *     model  MPCT_NMPC_VANDEVUSSE: nmpc_vandevusse_state.m (nx = 3, nu = 2), params[16] in the
+ *            order of nmpc_vandevusse_state.m:43-58 (k10 k20 k30 E1 E2 E3 dHab dHbc dHad rho cp
+ *            Kw Ar V T0 Ca0); NULL = the reference's values
+ *   xc[ny]          output states, 1-based as init.xc (VanDeVusse_NMPC.m:82: [2 3]); ny <= 2
+ *   ts, nsub        Ts and the fixed RK4 sub-steps per Ts that replace ode15s / the toolbox's
+ *                   discretisation (plant and prediction use the same integrator)
+ *   x0[nx], u0[nu]  init.x0, init.u0
+ *   u_min/u_max[nu] MV Min/Max (hard); x_min/x_max[nx] state bounds (reported through
+ *                   MPCT_ST_BOUNDS, not enforced); y_scale[ny], u_scale[nu] OV / MV ScaleFactor
+ *   n_max, nu_max   largest prediction / control horizon any candidate uses (nu*nu_max <= 32)
+ *   nit, yref[ny*nit], vns_ink  as in mpct_scenario_desc
+ *   sqp_max, sqp_tol  Gauss-Newton iteration cap per controller call and the stopping test
+ *                   max |change of an absolute move| / u_scale <= sqp_tol (0: 100 and 1e-8); each
+ *                   step is globalised by Armijo backtracking on the cost
+ * Evaluate with mpct_eval_batch(_device) exactly like a linear scenario: N2[] holds N, delta[] the
+ * OV weights, lambda[] the MVRate weights, r[] the reference sets (ny rows), v = NULL; ys / uopt
+ * are yopt / uopt; qp_iters counts Gauss-Newton iterations. */
+#define MPCT_NMPC_VANDEVUSSE 1
+typedef struct mpct_nmpc_desc {
+  int32_t abi_version; /* >= 4 */
+  int32_t model;
+  int32_t nx, ny, nu;
+  const double* params;
+  const int32_t* xc;
+  double ts;
+  int32_t nsub;
+  const double* x0;
+  const double* u0;
+  const double* u_min;
+  const double* u_max;
+  const double* x_min;
+  const double* x_max;
+  const double* y_scale;
+  const double* u_scale;
+  int32_t n_max, nu_max;
+  int32_t nit;
+  const double* yref;
+  int32_t vns_ink;
+  int32_t sqp_max;
+  double sqp_tol;
+} mpct_nmpc_desc;
+
+/* Build a nonlinear MPC scenario (no device needed).  Returns MPCT_OK. */
+int32_t mpct_nmpc_scenario_create(const mpct_nmpc_desc* desc, mpct_scenario** out);
 
 /* Evaluation options. */
 typedef struct mpct_opts {

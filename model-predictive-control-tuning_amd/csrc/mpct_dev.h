@@ -24,6 +24,12 @@ constexpr int MPCT_ST_QP_INFEAS_ = 2;
 constexpr int MPCT_ST_NONFINITE_ = 4;
 constexpr int MPCT_ST_SKIPPED_ = 8;
 constexpr int MPCT_ST_BADHORIZON_ = 16;
+constexpr int MPCT_ST_SQP_MAXITER_ = 32;
+constexpr int MPCT_ST_BOUNDS_ = 64;
+
+// NMPC model parameter table (mpct_nmpc_desc.params, nmpc_vandevusse_state.m:43-58 order)
+enum { NM_K10 = 0, NM_K20, NM_K30, NM_E1, NM_E2, NM_E3, NM_DAB, NM_DBC, NM_DAD, NM_RHO, NM_CP, NM_KW, NM_AR,
+       NM_V, NM_T0, NM_CA0, NM_NPAR };
 
 struct DevScenario {
   int my, nu, nd, nin, nit;
@@ -70,6 +76,12 @@ struct DevScenario {
   const double* step_md;  // [my][nd][tlen]  model MD step responses
   const double* obnd;     // [4][my]  y_min, y_max, MinECR*s_y, MaxECR*s_y (+-inf: no bound)
   const double* wscale;   // [my + nu]  1/s_y, 1/s_u (weights over ScaleFactors)
+  // nonlinear MPC (nmpc = 1, nmpc_kernel.hip): my = outputs, nu = MVs, n2max = largest N
+  int nmpc;
+  int nsub, sqp_max;
+  double ts, sqp_tol;
+  const int* xc;          // [my] output states (0-based)
+  const double* nm;       // [NM_NPAR][x0 3][u0 nu][u_min nu][u_max nu][x_min 3][x_max 3][s_y my][s_u nu]
 };
 
 struct DevOpts {

@@ -32,6 +32,11 @@ int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, c
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
                   hipStream_t stream, std::string* err);
 long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu);
+// defined in nmpc_kernel.hip
+int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
+                const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
+                std::string* err);
+long long nmpc_lds_bytes(int M);
 }  // namespace mpct
 
 using namespace mpct;
@@ -72,6 +77,11 @@ struct mpct_scenario {
   std::vector<double> step_md;  // [my][nd][tlen]
   std::vector<double> obnd;     // [4][my]
   std::vector<double> wscale;   // [my + nu]
+  // nonlinear MPC (abi >= 4, mpct_nmpc_scenario_create): my = ny outputs, nu MVs
+  int nmpc = 0, nsub = 10, sqp_max = 100;
+  double ts = 0.0, sqp_tol = 1e-8;
+  std::vector<int> xc;      // [ny] 0-based output states
+  std::vector<double> nm;   // see DevScenario::nm
   // device state
   int dev = -2;
   void* dtab = nullptr;
@@ -528,6 +538,65 @@ extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenar
   return MPCT_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// nonlinear MPC scenario (closedloop_toolbox_nmpc.m; VanDeVusse_NMPC.m)
+static const double kVdvParams[NM_NPAR] = {  // nmpc_vandevusse_state.m:43-58
+    1.287e12, 1.287e12, 9.043e9, -9758.3, -9758.3, -8560.0, -4.20, 11.00, 41.85,
+    0.9342,   3.01,     4032.0,  0.215,   10.0,    130.00,  5.10};
+
+extern "C" int32_t mpct_nmpc_scenario_create(const mpct_nmpc_desc* d, mpct_scenario** out) {
+  if (!d || !out) return fail(MPCT_EINVAL, "null argument");
+  *out = nullptr;
+  if (d->abi_version < 4 || d->abi_version > MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
+  if (d->model != MPCT_NMPC_VANDEVUSSE) return fail(MPCT_EINVAL, "unknown NMPC model id");
+  if (d->nx != 3 || d->nu != 2) return fail(MPCT_EINVAL, "the Van de Vusse model has nx = 3, nu = 2");
+  if (d->ny < 1 || d->ny > 2) return fail(MPCT_ERANGE, "ny must be 1 or 2");
+  if (d->nit < 1 || d->n_max < 1 || d->nu_max < 1) return fail(MPCT_EINVAL, "non-positive dimension");
+  if (d->nu * d->nu_max > 32) return fail(MPCT_ERANGE, "nu*nu_max > 32");
+  if (!(d->ts > 0.0) || d->nsub < 1) return fail(MPCT_EINVAL, "ts must be > 0 and nsub >= 1");
+  if (!d->xc || !d->x0 || !d->u0 || !d->u_min || !d->u_max || !d->x_min || !d->x_max || !d->y_scale ||
+      !d->u_scale || !d->yref)
+    return fail(MPCT_EINVAL, "null table pointer");
+  for (int j = 0; j < d->ny; ++j)
+    if (d->xc[j] < 1 || d->xc[j] > d->nx) return fail(MPCT_EINVAL, "xc out of range (1-based state index)");
+  for (int n = 0; n < d->nu; ++n) {
+    if (!(d->u_min[n] < d->u_max[n])) return fail(MPCT_EINVAL, "u_min must be < u_max");
+    if (!(d->u_scale[n] > 0.0)) return fail(MPCT_EINVAL, "u_scale must be > 0");
+  }
+  for (int j = 0; j < d->ny; ++j)
+    if (!(d->y_scale[j] > 0.0)) return fail(MPCT_EINVAL, "y_scale must be > 0");
+  auto* s = new mpct_scenario();
+  s->nmpc = 1;
+  s->my = d->ny;
+  s->nu = d->nu;
+  s->nd = 0;
+  s->npin = d->nu;
+  s->nit = d->nit;
+  s->n2max = d->n_max;
+  s->numax = d->nu_max;
+  s->ink0 = d->vns_ink > 0 ? d->vns_ink - 1 : 9;
+  s->nsub = d->nsub;
+  s->ts = d->ts;
+  s->sqp_max = d->sqp_max > 0 ? d->sqp_max : 100;
+  s->sqp_tol = d->sqp_tol > 0.0 ? d->sqp_tol : 1e-8;
+  for (int j = 0; j < d->ny; ++j) s->xc.push_back(d->xc[j] - 1);
+  const double* p = d->params ? d->params : kVdvParams;
+  s->nm.assign(p, p + NM_NPAR);
+  auto app = [&](const double* a, int n) { s->nm.insert(s->nm.end(), a, a + n); };
+  app(d->x0, 3);
+  app(d->u0, d->nu);
+  app(d->u_min, d->nu);
+  app(d->u_max, d->nu);
+  app(d->x_min, 3);
+  app(d->x_max, 3);
+  app(d->y_scale, d->ny);
+  app(d->u_scale, d->nu);
+  s->yref.assign(d->yref, d->yref + (size_t)d->ny * d->nit);
+  *out = s;
+  g_err.clear();
+  return MPCT_OK;
+}
+
 extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
   if (!s) return;
   if (s->dtab || s->dscratch) {
@@ -614,6 +683,8 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   size_t o_smd = put(s->step_md.data(), s->step_md.size() * 8);
   size_t o_obnd = put(s->obnd.data(), s->obnd.size() * 8);
   size_t o_wsc = put(s->wscale.data(), s->wscale.size() * 8);
+  size_t o_xc = put(s->xc.data(), s->xc.size() * 4);
+  size_t o_nm = put(s->nm.data(), s->nm.size() * 8);
   void* dp = nullptr;
   if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
   if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -639,7 +710,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
   {
-    bool rp = !s->mdband && s->pl_maxa - 1 <= kRegA;  // gpc_kernel.hip only
+    bool rp = !s->mdband && !s->nmpc && s->pl_maxa - 1 <= kRegA;  // gpc_kernel.hip only
     for (int e = 0; e < s->nvar * s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
     for (int n = 0; rp && n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
     for (int i = 0; rp && i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
@@ -677,6 +748,13 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.step_md = reinterpret_cast<const double*>(b + o_smd);
   ds.obnd = reinterpret_cast<const double*>(b + o_obnd);
   ds.wscale = reinterpret_cast<const double*>(b + o_wsc);
+  ds.nmpc = s->nmpc;
+  ds.nsub = s->nsub;
+  ds.sqp_max = s->sqp_max;
+  ds.ts = s->ts;
+  ds.sqp_tol = s->sqp_tol;
+  ds.xc = reinterpret_cast<const int*>(b + o_xc);
+  ds.nm = reinterpret_cast<const double*>(b + o_nm);
   s->dtab = dp;
   s->dev = dev;
   return MPCT_OK;
@@ -723,10 +801,13 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   dr.prof = dprof;
 #endif
   std::string err;
-  rc = s->mdband ? launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr,
-                                 static_cast<hipStream_t>(stream), &err)
-                 : launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
-                                      static_cast<hipStream_t>(stream), &err);
+  if (s->nmpc)
+    rc = launch_nmpc(s->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, static_cast<hipStream_t>(stream), &err);
+  else if (s->mdband)
+    rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream), &err);
+  else
+    rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
+                            static_cast<hipStream_t>(stream), &err);
   if (rc) return fail(rc, err);
 #ifdef MPCT_PROFILE
   {
@@ -831,6 +912,7 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
 
 extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {
   if (!s) return fail(MPCT_EINVAL, "null scenario");
+  if (s->nmpc) return nmpc_lds_bytes(s->nu * Nu);
   DevScenario ds{};
   ds.my = s->my;
   ds.nu = s->nu;

@@ -1,0 +1,577 @@
+// nmpc_kernel.hip — batched closed loop of the nonlinear MPC of VanDeVusse_NMPC.m (config 5), one
+// wavefront (64 lanes) per simulation.
+//
+// Replaces, per simulation, closedloop_toolbox_nmpc.m:36-97: nlmpcmove at every step of an
+// nit-step closed loop on the Van de Vusse reactor (nmpc_vandevusse_state.m:64-82), plus the
+// open-loop prediction from (x0, u0) at r(:,end).  The closed-source parts are replaced as in
+// oracle/nmpc_vdv.py: one fixed-step RK4 (nsub sub-steps per Ts) for plant and
+// prediction; nlmpc's fmincon SQP by single-shooting Gauss-Newton SQP on the documented standard
+// cost  sum (w_y/s_y)^2 (y - r)^2 + sum (w_du/s_u)^2 du^2  with hard MV bounds.
+//
+// Device formulation: decision variables are the move increments v = dU (lane m = n*Nu + l),
+// so the rate term is diagonal and the MV bounds are gi_core's box rows (kind 0/1 at l = 0,
+// cumulative kind 2/3 at l > 0).  Each Gauss-Newton iteration:
+//   * lanes integrate the prediction x(k+1..k+N) redundantly and carry their own tangent
+//     dx/dv_m through the RK4 stages (forward-mode sensitivities, exact for the RK4 map);
+//   * every predicted output row (w_y dy/dv | w_y (y - r)) is streamed into a row-wise Givens QR
+//     of the least-squares Jacobian as soon as it is produced (lanes = columns, lane M = the
+//     residual column): no Jacobian is stored, and the QP never sees normal equations (the rate
+//     weights span 1e-11..1 against the output rows' 1e2: cond(H) ~ 1e15, cond(R) ~ 3e7);
+//   * the step solves the box QP with the Goldfarb-Idnani dual method of gi_core.h (J = R^-1);
+//   * v += step; stop when the largest absolute-move change / s_u <= sqp_tol (the oracle's test).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "gi_core.h"
+#include "mpct_dev.h"
+
+namespace mpct {
+
+// Van de Vusse model constants, derived once per wave from the parameter table
+struct VdV {
+  double k10, k20, k30, e1, e2, e3, dab, dbc, dad, a, b, T0, ca0;
+};
+
+__device__ __forceinline__ VdV vdv_load(const double* p) {
+  VdV P;
+  P.k10 = p[NM_K10];
+  P.k20 = p[NM_K20];
+  P.k30 = p[NM_K30];
+  P.e1 = p[NM_E1];
+  P.e2 = p[NM_E2];
+  P.e3 = p[NM_E3];
+  P.dab = p[NM_DAB];
+  P.dbc = p[NM_DBC];
+  P.dad = p[NM_DAD];
+  P.a = 1.0 / (p[NM_RHO] * p[NM_CP]);
+  P.b = p[NM_KW] * p[NM_AR] / (p[NM_RHO] * p[NM_CP] * p[NM_V]);
+  P.T0 = p[NM_T0];
+  P.ca0 = p[NM_CA0];
+  return P;
+}
+
+// state derivative f(x, u) (nmpc_vandevusse_state.m:64-82) and, with TAN, its directional
+// derivative along (xd, ud)
+template <bool TAN>
+__device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const double u[2], const double xd[3],
+                                        const double ud[2], double f[3], double fd[3]) {
+  const double ca = x[0], cb = x[1], T = x[2];
+  const double th = T + 273.15;
+  const double ith = 1.0 / th;
+  const double k1 = P.k10 * exp(P.e1 * ith);
+  const double k2 = P.k20 * exp(P.e2 * ith);
+  const double k3 = P.k30 * exp(P.e3 * ith);
+  const double fov = u[0], tk = u[1];
+  f[0] = fov * (P.ca0 - ca) - k1 * ca - k3 * ca * ca;
+  f[1] = -fov * cb + k1 * ca - k2 * cb;
+  f[2] = P.a * (k1 * ca * P.dab + k2 * cb * P.dbc + k3 * ca * ca * P.dad) + fov * (P.T0 - T) + P.b * (tk - T);
+  if (TAN) {
+    const double ith2 = ith * ith;
+    const double Td = xd[2];
+    const double k1d = -P.e1 * ith2 * k1 * Td, k2d = -P.e2 * ith2 * k2 * Td, k3d = -P.e3 * ith2 * k3 * Td;
+    const double cad = xd[0], cbd = xd[1];
+    fd[0] = ud[0] * (P.ca0 - ca) - fov * cad - k1d * ca - k1 * cad - k3d * ca * ca - 2.0 * k3 * ca * cad;
+    fd[1] = -ud[0] * cb - fov * cbd + k1d * ca + k1 * cad - k2d * cb - k2 * cbd;
+    fd[2] = P.a * (k1d * ca * P.dab + k1 * cad * P.dab + k2d * cb * P.dbc + k2 * cbd * P.dbc + k3d * ca * ca * P.dad +
+                   2.0 * k3 * ca * cad * P.dad) +
+            ud[0] * (P.T0 - T) - fov * Td + P.b * (ud[1] - Td);
+  }
+}
+
+// one sample Ts of classical RK4 with nsub sub-steps (oracle/nmpc_vdv.py rk4), tangent optional
+template <bool TAN>
+__device__ __forceinline__ void vdv_rk4(const VdV& P, double h, int nsub, double x[3], const double u[2],
+                                        double xd[3], const double ud[2]) {
+  for (int s = 0; s < nsub; ++s) {
+    double k1[3], k2[3], k3[3], k4[3], K1[3], K2[3], K3[3], K4[3], xs[3], Xs[3];
+    vdv_rhs<TAN>(P, x, u, xd, ud, k1, K1);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      xs[i] = x[i] + 0.5 * h * k1[i];
+      if (TAN) Xs[i] = xd[i] + 0.5 * h * K1[i];
+    }
+    vdv_rhs<TAN>(P, xs, u, Xs, ud, k2, K2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      xs[i] = x[i] + 0.5 * h * k2[i];
+      if (TAN) Xs[i] = xd[i] + 0.5 * h * K2[i];
+    }
+    vdv_rhs<TAN>(P, xs, u, Xs, ud, k3, K3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      xs[i] = x[i] + h * k3[i];
+      if (TAN) Xs[i] = xd[i] + h * K3[i];
+    }
+    vdv_rhs<TAN>(P, xs, u, Xs, ud, k4, K4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      x[i] = x[i] + (h / 6.0) * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+      if (TAN) xd[i] = xd[i] + (h / 6.0) * (K1[i] + 2.0 * K2[i] + 2.0 * K3[i] + K4[i]);
+    }
+  }
+}
+
+__device__ __forceinline__ double sel3(const double x[3], int i) { return i == 0 ? x[0] : (i == 1 ? x[1] : x[2]); }
+
+// Gauss-Newton globalisation (oracle/nmpc_vdv.py LS_MAX, LS_C1, LS_FLAT)
+constexpr int kLsMax = 12;
+constexpr double kLsC1 = 1e-4;
+constexpr double kLsFlat = 1e-14;
+
+// LDS layout (doubles) of one simulation at QP size M
+struct NmLayout {
+  int ri, jt, ra, rr, dv, xc, u, uo, rw, cv, total;
+};
+__host__ __device__ inline NmLayout nm_layout(int M) {
+  NmLayout L;
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
+  L.ri = take(M * M);
+  L.jt = take(M * M);
+  L.ra = take(M * M);
+  L.rr = take(M * M);  // R of the Gauss-Newton least-squares QR (row-major, upper)
+  L.dv = take(M + 1);
+  L.xc = take(M + 1);
+  L.u = take(M + 1);   // absolute moves of the current iterate
+  L.uo = take(M + 1);  // absolute moves of the open-loop solution (Info.MVopt)
+  L.rw = take(M + 1);  // rate residuals w_u v of the current iterate
+  L.cv = take(M + 1);  // c = Q'r, the rotated residual
+  L.total = (o + 1) & ~1;
+  return L;
+}
+
+template <int MAXM>
+__global__ void __launch_bounds__(64, 1)
+    nmpc_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ Nv,
+                            const int* __restrict__ Nuv, const double* __restrict__ deltav,
+                            const double* __restrict__ lambdav, const double* __restrict__ rv, const DevOpts o,
+                            const DevResult out, int mz_lo) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x;
+  const long long sim = blockIdx.x;
+  if (sim >= C * nref) return;
+  const long long c = sim / nref;
+  const int kref = (int)(sim - c * nref);
+  const int ny = sc.my, nu = sc.nu, nit = sc.nit;
+  const int N = Nv[c], Nu = Nuv[c];
+  const int M = nu * Nu;
+  int st = 0;
+
+  auto write_nan = [&](int status) __attribute__((always_inline)) {
+    if (lane < ny) {
+      if (out.J1) out.J1[sim * ny + lane] = NAN;
+      if (out.j21) out.j21[sim * ny + lane] = NAN;
+      if (out.j22) out.j22[sim * ny + lane] = NAN;
+    }
+    if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = NAN;
+    if (lane == 0) {
+      if (out.status) out.status[sim] = status;
+      if (out.qp_iters) out.qp_iters[sim] = 0;
+    }
+  };
+  const bool first = mz_lo == 0;
+  if (N <= 0) {
+    if (first) write_nan(MPCT_ST_SKIPPED_);
+    return;
+  }
+  if (N > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N) {
+    if (first) write_nan(MPCT_ST_BADHORIZON_);
+    return;
+  }
+  if (M <= mz_lo || M > MAXM) return;  // another launch's QP size class
+  const NmLayout L = nm_layout(M);
+  double* sRi = lds + L.ri;
+  double* sJT = lds + L.jt;
+  double* sRA = lds + L.ra;
+  double* sd = lds + L.dv;
+  double* sxc = lds + L.xc;
+  double* sU = lds + L.u;
+  double* sUo = lds + L.uo;
+  double* srw = lds + L.rw;
+  double* sR = lds + L.rr;
+  double* scv = lds + L.cv;
+
+  const double* tab = sc.nm;  // [params][x0 3][u0 nu][lb nu][ub nu][xmin 3][xmax 3][sy ny][su nu]
+  const VdV P = vdv_load(tab);
+  const double* tx0 = tab + NM_NPAR;
+  const double* tu0 = tx0 + 3;
+  const double* tlb = tu0 + nu;
+  const double* tub = tlb + nu;
+  const double* txmin = tub + nu;
+  const double* txmax = txmin + 3;
+  const double* tsy = txmax + 3;
+  const double* tsu = tsy + ny;
+  const double h = sc.ts / sc.nsub;
+  const int nsub = sc.nsub;
+
+  const bool row = lane < M;
+  const int bn = row ? lane / Nu : 0;     // MV of this lane's move
+  const int bl = row ? lane - bn * Nu : 0;  // move index within the block
+  const double lbn = tlb[bn], ubn = tub[bn], sun = tsu[bn];
+  // toolbox weights over ScaleFactors, squared in the cost: residual rows carry w = |weight|/s
+  const double* dl = deltav + c * ny;
+  const double* lm = lambdav + c * nu;
+  const double wu = fabs(lm[bn]) / sun;
+  int xc0 = sc.xc[0], xc1 = ny > 1 ? sc.xc[1] : 0;
+  const double wy0 = fabs(dl[0]) / tsy[0], wy1 = ny > 1 ? fabs(dl[1]) / tsy[1] : 0.0;
+  const double tol = o.feas_tol;
+  const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 200 * M + 1000;
+  const double* rr = rv + (long long)kref * ny * nit;
+  long long sqp_total = 0;
+
+  // ---- one controller call (nlmpcmove restated): Gauss-Newton SQP from the warm start v
+  // (this lane's increment), state x, last move ul[n], reference (r0, r1).  Returns v.
+  auto controller = [&](const double x[3], const double ul[2], double r0, double r1, double v)
+                        __attribute__((always_inline)) -> double {
+    for (int it = 0; it < sc.sqp_max; ++it) {
+      ++sqp_total;
+      // absolute moves of the iterate: U[n][l] = ul[n] + sum_{l' <= l} v[n][l']
+      if (row) sxc[lane] = v;
+      lds_sync();
+      double cum = 0.0;
+      if (row) {
+        for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
+        sU[lane] = (bn == 0 ? ul[0] : ul[1]) + cum;
+        srw[lane] = wu * v;
+      }
+      lds_sync();
+      // ---- least-squares Jacobian [rate rows; output rows] by row-streamed Givens QR
+      double rcol[MAXM];
+#pragma unroll
+      for (int k = 0; k < MAXM; ++k) {
+        double e = 0.0;
+        if (k < M) {
+          if (lane == k) e = wu;
+          else if (lane == M) e = srw[k];  // rate residual w_u v_k
+        }
+        rcol[k] = e;
+      }
+      double xs[3] = {x[0], x[1], x[2]};
+      double td[3] = {0.0, 0.0, 0.0};
+      double fo = 0.0;  // sum of squared output residuals (lane M)
+      for (int i = 0; i < N; ++i) {
+        const int li = i < Nu - 1 ? i : Nu - 1;
+        const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
+        double ud[2] = {0.0, 0.0};
+        if (row && bl <= li) ud[bn] = 1.0;
+        vdv_rk4<true>(P, h, nsub, xs, u, td, ud);
+        for (int j = 0; j < ny; ++j) {
+          const int xj = j == 0 ? xc0 : xc1;
+          const double wy = j == 0 ? wy0 : wy1;
+          if (!(wy > 0.0)) continue;
+          double w = 0.0;
+          if (row) w = wy * sel3(td, xj);
+          else if (lane == M) w = wy * (sel3(xs, xj) - (j == 0 ? r0 : r1));
+          fo += w * w;
+#pragma unroll
+          for (int k = 0; k < MAXM; ++k) {
+            if (k < M) {
+              const double b = bcast(w, k);
+              const double a = bcast(rcol[k], k);
+              const double rho = sqrt(a * a + b * b);
+              const bool nz = b != 0.0;
+              const double cs = nz ? a / rho : 1.0, sn = nz ? b / rho : 0.0;
+              const double rk = rcol[k];
+              rcol[k] = cs * rk + sn * w;
+              w = -sn * rk + cs * w;
+            }
+          }
+        }
+      }
+      // R (upper, lane j holds column j) and c = Q'r (lane M) -> LDS
+      if (row || lane == M) {
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+          if (k < M) {
+            if (row) sR[k * M + lane] = rcol[k];
+            else scv[k] = rcol[k];
+          }
+      }
+      const double f0 = 0.5 * (bcast(fo, M) + qsum<MAXM>(row ? (wu * v) * (wu * v) : 0.0));
+      lds_sync();
+      // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
+      if (row) {
+        for (int kk = lane; kk >= 0; --kk) {
+          double a = (kk == lane) ? 1.0 : 0.0;
+          for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[j * M + lane];
+          sRi[kk * M + lane] = a / sR[kk * M + kk];
+        }
+        for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
+      }
+      lds_sync();
+      // unconstrained Gauss-Newton step s_u = -R^-1 c
+      double xm = 0.0;
+      if (row)
+        for (int k = lane; k < M; ++k) xm -= sRi[lane * M + k] * scv[k];
+      // ---- box QP: lb <= U + cumulative step <= ub, Goldfarb-Idnani from s_u
+      const double clo = row ? lbn - sU[lane] : 0.0, chi = row ? ubn - sU[lane] : 0.0;
+      lds_sync();
+      GIState<MAXM> gis;
+      gi_reset<MAXM>(gis);
+      gi_load_rinv<MAXM>(gis, sJT, sRi, M, row);
+      int git = 0;
+      for (;;) {
+        const double pre = block_prefix<MAXM>(xm, bl, Nu, row, sxc);
+        double s4[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+        if (row) {
+          if (bl == 0) {
+            s4[0] = xm - clo;
+            s4[1] = chi - xm;
+          } else {
+            s4[2] = pre - clo;
+            s4[3] = chi - pre;
+          }
+        }
+        double best = INFINITY;
+        int bid = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (!((gis.act >> k) & 1u) && s4[k] < best) {
+            best = s4[k];
+            bid = 4 * lane + k;
+          }
+        wave_argmin64(best, bid);
+        if (!(best < -tol)) break;
+        if (git >= maxit) {
+          st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
+        const int p = bid;
+        double sp = best, upm = 0.0;
+        bool infeas = false;
+        for (;;) {
+          ++git;
+          const CInfo ci = cinfo(p, Nu);
+          const double dk = gi_dvec<MAXM>(sJT, sd, M, ci.j0, ci.j1, ci.sg, row);
+          lds_sync();
+          const double d2 = row ? dk * dk : 0.0;
+          const double dn2 = qsum<MAXM>(d2);
+          const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
+          const double zm = gi_z(sJT, sd, gis.q, M, row);
+          const double rk = gi_backsub<MAXM>(gis, sRA, M, dk);
+          double t1 = INFINITY;
+          int kdrop = 0x7fffffff;
+          if (lane < gis.q && rk > 0.0) {
+            t1 = gis.uw / rk;
+            kdrop = lane;
+          }
+          qargmin<MAXM>(t1, kdrop);
+          const double t2 = (beta > 1e-20 * dn2) ? -sp / beta : INFINITY;
+          if (t1 == INFINITY && t2 == INFINITY) {
+            st |= MPCT_ST_QP_INFEAS_;
+            infeas = true;
+            break;
+          }
+          const bool full = t2 <= t1;
+          const double t = full ? t2 : t1;
+          if (t2 != INFINITY) xm += t * zm;
+          if (lane < gis.q) gis.uw -= t * rk;
+          upm += t;
+          sp += t * beta;
+          if (full) {
+            gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
+            break;
+          }
+          gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, BoxMark{});
+          if (git >= maxit) break;
+        }
+        if (infeas) break;
+        if (git >= maxit) {
+          st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
+      }
+      // ---- convergence on the absolute-move change of the full step (oracle: max|d|/s_u)
+      const double dpre = block_prefix<MAXM>(xm, bl, Nu, row, sxc);
+      double chg = row ? fabs(dpre) / sun : 0.0;
+      if (!isfinite(chg)) chg = INFINITY;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) chg = fmax(chg, __shfl_xor(chg, off, 64));
+      if (chg <= sc.sqp_tol) return v + (row ? xm : 0.0);
+      if (!(chg < INFINITY)) {
+        st |= MPCT_ST_NONFINITE_;
+        return v;
+      }
+      // ---- Armijo backtracking on the cost along the step (oracle/nmpc_vdv.py controller):
+      // dd = r'J s = c'R s, then halve alpha until f(v + alpha s) <= f0 + c1 alpha dd or the
+      // cost change is below its own rounding; the last alpha is taken regardless
+      if (row) sxc[lane] = xm;
+      lds_sync();
+      double rs = 0.0;
+      if (row)
+        for (int j = lane; j < M; ++j) rs += sR[lane * M + j] * sxc[j];
+      const double dd = qsum<MAXM>(row ? scv[lane] * rs : 0.0);
+      double alpha = 1.0;
+      for (int ls = 0; ls < kLsMax; ++ls) {
+        const double va = v + (row ? alpha * xm : 0.0);
+        lds_sync();
+        if (row) sxc[lane] = va;
+        lds_sync();
+        if (row) {
+          double cum = 0.0;
+          for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
+          sU[lane] = (bn == 0 ? ul[0] : ul[1]) + cum;
+        }
+        lds_sync();
+        double xa[3] = {x[0], x[1], x[2]};
+        double fa = 0.0;
+        for (int i = 0; i < N; ++i) {
+          const int li = i < Nu - 1 ? i : Nu - 1;
+          const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
+          vdv_rk4<false>(P, h, nsub, xa, u, nullptr, nullptr);
+          const double e0 = wy0 * (sel3(xa, xc0) - r0);
+          fa += e0 * e0;
+          if (ny > 1) {
+            const double e1 = wy1 * (sel3(xa, xc1) - r1);
+            fa += e1 * e1;
+          }
+        }
+        const double f1 = 0.5 * (fa + qsum<MAXM>(row ? (wu * va) * (wu * va) : 0.0));
+        if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) break;
+        alpha *= 0.5;
+      }
+      v += row ? alpha * xm : 0.0;
+    }
+    st |= MPCT_ST_SQP_MAXITER_;
+    return v;
+  };
+
+  // ------------------------------------------------------------------ open-loop prediction
+  // closedloop_toolbox_nmpc.m:79-95: one call at (x0, u0, r(:,end)); MVopt held after Nu
+  double x0[3] = {tx0[0], tx0[1], tx0[2]};
+  double u0[2] = {tu0[0], nu > 1 ? tu0[1] : 0.0};
+  double vop = 0.0;
+  double jnu = 0.0;
+  if (o.open_loop) {
+    vop = controller(x0, u0, ny > 0 ? rr[nit - 1] : 0.0, ny > 1 ? rr[nit + nit - 1] : 0.0, 0.0);
+    // absolute moves -> sU (held in LDS for the open-loop simulation)
+    if (row) sxc[lane] = vop;
+    lds_sync();
+    if (row) {
+      double cum = 0.0;
+      for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
+      sUo[lane] = u0[bn] + cum;
+    }
+    lds_sync();
+    if (lane < nu) {
+      // VNS2.m:183-191: Xnu = |uopt(:,1)| ./ |diff(uopt)|, inf/NaN -> 0, Jnu = sum Xnu^2;
+      // uopt(:,k) = MVopt row k (held after Nu - 1), k = 1..nit
+      const double uf = fabs(sUo[lane * Nu]);
+      for (int t = 0; t + 1 < nit; ++t) {
+        const int l0 = t < Nu - 1 ? t : Nu - 1, l1 = t + 1 < Nu - 1 ? t + 1 : Nu - 1;
+        const double dd = fabs(sUo[lane * Nu + l1] - sUo[lane * Nu + l0]);
+        const double xr = uf / dd;
+        if (isfinite(xr)) jnu += xr * xr;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ closed loop
+  double x[3] = {x0[0], x0[1], x0[2]};
+  double xo[3] = {x0[0], x0[1], x0[2]};
+  double ul[2] = {u0[0], u0[1]};
+  double v = 0.0;  // warm start: moves held at u0
+  double j1 = 0.0, j21 = 0.0, j22 = 0.0;
+  bool inb = true;
+  const int ink0 = sc.ink0;
+  for (int t = 0; t < nit; ++t) {
+    if (t > 0) {
+      const double r0 = rr[t], r1 = ny > 1 ? rr[nit + t] : 0.0;
+      v = controller(x, ul, r0, r1, v);
+      // the first move U(:,t) = u(t-1) + v[n][0]
+      if (row) sxc[lane] = v;
+      lds_sync();
+      double un[2] = {ul[0] + sxc[0], nu > 1 ? ul[1] + sxc[Nu] : 0.0};
+      lds_sync();
+      vdv_rk4<false>(P, h, nsub, x, un, nullptr, nullptr);
+      ul[0] = un[0];
+      ul[1] = un[1];
+      // warm start for the next step: the solution shifted by one move (last move repeated),
+      // expressed against the new last move: v'[l] = v[l+1], v'[Nu-1] = 0
+      const double vn = lane_next<64>(v);
+      v = (row && bl < Nu - 1) ? vn : 0.0;
+      if (o.open_loop) {
+        const int l = t < Nu - 1 ? t : Nu - 1;
+        const double uo[2] = {sUo[l], nu > 1 ? sUo[Nu + l] : 0.0};
+        vdv_rk4<false>(P, h, nsub, xo, uo, nullptr, nullptr);
+      }
+    }
+    for (int i = 0; i < 3; ++i) inb = inb && x[i] >= txmin[i] - 1e-9 && x[i] <= txmax[i] + 1e-9;
+    if (lane < ny) {
+      const double y = sel3(x, lane == 0 ? xc0 : xc1);
+      const double e1 = y - sc.yref[lane * nit + t];
+      j1 += e1 * e1;
+      if (t >= ink0) j22 += e1 * e1;
+      double ysv = 0.0;
+      if (o.open_loop) {
+        ysv = sel3(xo, lane == 0 ? xc0 : xc1);
+        if (t >= ink0) j21 += (y - ysv) * (y - ysv);
+      }
+      if (o.want_traj) {
+        if (out.y) out.y[(sim * ny + lane) * nit + t] = y;
+        if (o.open_loop && out.ys) out.ys[(sim * ny + lane) * nit + t] = ysv;
+      }
+    }
+    if (o.want_traj && lane < nu) {
+      if (out.u) out.u[(sim * nu + lane) * nit + t] = ul[lane == 0 ? 0 : 1];
+      if (o.open_loop && out.uopt) {
+        const int l = t < Nu - 1 ? t : Nu - 1;
+        out.uopt[(sim * nu + lane) * nit + t] = sUo[lane * Nu + l];
+      }
+    }
+  }
+  if (!inb) st |= MPCT_ST_BOUNDS_;
+  // ------------------------------------------------------------------ results
+  if (lane < ny) {
+    if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;
+    if (out.J1) out.J1[sim * ny + lane] = j1;
+    if (out.j22) out.j22[sim * ny + lane] = j22;
+    if (out.j21) out.j21[sim * ny + lane] = o.open_loop ? j21 : NAN;
+  }
+  if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = o.open_loop ? jnu : NAN;
+  const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
+  if (lane == 0) {
+    const int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
+    if (out.status) out.status[sim] = s;
+    if (out.qp_iters) out.qp_iters[sim] = sqp_total;
+  }
+}
+
+}  // namespace mpct
+
+// ------------------------------------------------------------------------------------------
+// host-side launch
+#include <string>
+
+namespace mpct {
+
+long long nmpc_lds_bytes(int M) { return (long long)nm_layout(M).total * 8; }
+
+// one launch per QP size class (MAXM 16 / 32); a simulation runs in the launch of its class
+int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
+                const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
+                std::string* err) {
+  const int Mmax = sc.nu * sc.numax;
+  if (Mmax > 32) {
+    *err = "nu*nu_max > 32";
+    return -4;
+  }
+  {
+    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax);
+    hipLaunchKernelGGL(nmpc_closed_loop_kernel<16>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream,
+                       sc, C, nref, N, Nu, delta, lambda, r, o, out, 0);
+  }
+  if (Mmax > 16) {
+    const long long lds = nmpc_lds_bytes(Mmax);
+    hipLaunchKernelGGL(nmpc_closed_loop_kernel<32>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream,
+                       sc, C, nref, N, Nu, delta, lambda, r, o, out, 16);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
+    return -3;
+  }
+  return 0;
+}
+
+}  // namespace mpct

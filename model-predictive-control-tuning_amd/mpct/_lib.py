@@ -54,6 +54,22 @@ class MpctScenarioDesc(C.Structure):
     ]
 
 
+class MpctNmpcDesc(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("model", C.c_int32),
+        ("nx", C.c_int32), ("ny", C.c_int32), ("nu", C.c_int32),
+        ("params", c_double_p), ("xc", c_int32_p),
+        ("ts", C.c_double), ("nsub", C.c_int32),
+        ("x0", c_double_p), ("u0", c_double_p),
+        ("u_min", c_double_p), ("u_max", c_double_p),
+        ("x_min", c_double_p), ("x_max", c_double_p),
+        ("y_scale", c_double_p), ("u_scale", c_double_p),
+        ("n_max", C.c_int32), ("nu_max", C.c_int32),
+        ("nit", C.c_int32), ("yref", c_double_p), ("vns_ink", C.c_int32),
+        ("sqp_max", C.c_int32), ("sqp_tol", C.c_double),
+    ]
+
+
 class MpctOpts(C.Structure):
     _fields_ = [("open_loop", C.c_int32), ("want_traj", C.c_int32), ("max_qp_iter", C.c_int32),
                 ("device", C.c_int32), ("feas_tol", C.c_double)]
@@ -68,10 +84,13 @@ class MpctResult(C.Structure):
 EXPORTS = [
     "mpct_abi_version", "mpct_last_error", "mpct_scenario_create", "mpct_scenario_destroy",
     "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
+    "mpct_nmpc_scenario_create",
 ]
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 ST_QP_MAXITER, ST_QP_INFEAS, ST_NONFINITE, ST_SKIPPED, ST_BADHORIZON = 1, 2, 4, 8, 16
+ST_SQP_MAXITER, ST_BOUNDS = 32, 64
+NMPC_VANDEVUSSE = 1
 
 _lib = None
 
@@ -105,6 +124,8 @@ def load():
     lib.mpct_last_error.restype = C.c_char_p
     lib.mpct_scenario_create.argtypes = [C.POINTER(MpctScenarioDesc), C.POINTER(C.c_void_p)]
     lib.mpct_scenario_create.restype = C.c_int32
+    lib.mpct_nmpc_scenario_create.argtypes = [C.POINTER(MpctNmpcDesc), C.POINTER(C.c_void_p)]
+    lib.mpct_nmpc_scenario_create.restype = C.c_int32
     lib.mpct_scenario_destroy.argtypes = [C.c_void_p]
     lib.mpct_scenario_destroy.restype = None
     lib.mpct_scenario_table.argtypes = [C.c_void_p, C.c_int32, c_double_p, C.c_int64]
