@@ -25,13 +25,13 @@
 #include "gi_core.h"
 
 #ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 1
+#define MPCT_WAVES_PER_EU 3  // 168 VGPRs: 3 waves per SIMD, which the trimmed LDS (13.4 KB at Shell 3x3) allows
 #endif
 namespace mpct {
 
 struct LdsLayout {
   int rinv, jt, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb, mza,
-      frb, fra, step, total;
+      frb, fra, total;
 };
 
 // LDS layout of one simulation; [x, plb) holds the state and every history (zeroed at start)
@@ -54,7 +54,7 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   L.yprev = take(my);
   L.ucum = take(M);
   L.ye = take(2 * ne);
-  L.yeh = take(2 * ne * kYeHist);
+  L.yeh = take(sc.regpath ? 0 : 2 * ne * kYeHist);  // register-resident histories need none
   L.uring = take(2 * nin * kURing);
   L.mzh = take(nmz * kYeHist);   // DTC: model entry output histories
   L.smz = take(nmz);             // DTC: model entry outputs of the step
@@ -65,7 +65,6 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   L.mza = take(nmz * (sc.dtc ? sc.mz_maxa : 0));
   L.frb = take(nfr * (sc.dtc ? sc.fr_max : 0));
   L.fra = take(nfr * (sc.dtc ? sc.fr_max : 0));
-  L.step = take(my * nu * sc.tlen > M * M ? my * nu * sc.tlen : M * M);  // prologue only
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -344,10 +343,8 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   double* sur = lds + L.uring;
   double* splb = lds + L.plb;
   double* spla = lds + L.pla;
-  double* sstep = lds + L.step;
 
   // ------------------------------------------------------------------ prologue
-  for (int e = lane; e < my * nu * sc.tlen; e += kWave) sstep[e] = sc.step[e];
   // this simulation's plant variant (Monte-Carlo draw k % nvar)
   const int pvar = sc.nvar > 1 ? kref % sc.nvar : 0;
   const int pve = pvar * ne;
@@ -418,7 +415,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       double v = 0.0;
       if (lane < M) {
         const int tt = sc.n1[i] + r - gc;
-        v = tt >= 0 ? sstep[(i * nu + gn) * sc.tlen + tt] : 0.0;
+        v = tt >= 0 ? sc.step[(i * nu + gn) * sc.tlen + tt] : 0.0;  // prologue only: global (L2)
       } else if (vlane) {
         v = sc.phi[(long long)(i * sc.n2max + r) * nx + vc];
       }
@@ -820,7 +817,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
 #include <string>
 
 #ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 1
+#define MPCT_WAVES_PER_EU 3  // 168 VGPRs: 3 waves per SIMD, which the trimmed LDS (13.4 KB at Shell 3x3) allows
 #endif
 namespace mpct {
 

@@ -26,6 +26,7 @@
 #include <math.h>
 
 #include "gi_core.h"
+#include "launch_fan.h"
 #include "mpct_dev.h"
 
 namespace mpct {
@@ -805,10 +806,12 @@ long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu) {
 // launch spans the whole batch; a simulation runs in the one launch whose class holds its
 // (Mz, LDS bytes) and leaves the others at once (no host round trip to bucket device-resident
 // candidates).  Status-only outcomes (padding, bad horizons) are written by the first launch.
+// Heaviest classes first, fanned over the caller's stream and the auxiliary streams of `fan`
+// (launch_fan.h): light classes fill the SIMDs a 1-workgroup-per-CU class leaves idle.
 template <int MAXM>
 static int launch_band_t(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                          const double* delta, const double* lambda, const double* r, const double* v,
-                         const DevOpts& o, const DevResult& out, hipStream_t stream, int mz_lo, bool& first,
+                         const DevOpts& o, const DevResult& out, FanScope& fs, int& nl, int mz_lo, bool& first,
                          std::string* err) {
   const int nu_hi = std::min(sc.numax, (MAXM - 1) / sc.nu);
   if (nu_hi < 1) return 0;
@@ -819,9 +822,15 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
   }
   auto kern = mdband_closed_loop_kernel<MAXM>;
   static const long long caps[4] = {40 * 1024, 53 * 1024, 80 * 1024, 160 * 1024};  // 4/3/2/1 per CU
-  long long lo = 0;
-  for (int k = 0; k < 4 && lo < lds_max; ++k) {
-    const long long lds = std::min(caps[k], lds_max);
+  long long lo[4], hi[4];
+  int ncls = 0;
+  for (long long l = 0; ncls < 4 && l < lds_max; ++ncls) {
+    lo[ncls] = l;
+    hi[ncls] = std::min(caps[ncls], lds_max);
+    l = hi[ncls];
+  }
+  for (int k = ncls - 1; k >= 0; --k) {
+    const long long lds = hi[k];
     if (lds > 64 * 1024) {
       if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds) != hipSuccess) {
@@ -829,31 +838,34 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
         return -3;
       }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
-                       delta, lambda, r, v, o, out, mz_lo, lo, lds, first ? 1 : 0);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, fs.stream(nl++), sc, C, nref, N2,
+                       Nu, delta, lambda, r, v, o, out, mz_lo, lo[k], lds, first ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
       return -3;
     }
     first = false;
-    lo = lds;
   }
   return 0;
 }
 
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
-                  hipStream_t stream, std::string* err) {
+                  hipStream_t stream, LaunchFan* fan, std::string* err) {
   const int Mz = sc.nu * sc.numax + 1;
   if (Mz > 64) {
     *err = "nu*nu_max + 1 > 64";
     return -4;
   }
+  FanScope fs(fan, stream);
   bool first = true;
-  int rc = launch_band_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 0, first, err);
-  if (rc == 0 && Mz > 16) rc = launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 16, first, err);
-  if (rc == 0 && Mz > 32) rc = launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, stream, 32, first, err);
+  int nl = 0, rc = 0;
+  if (Mz > 32) rc = launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, fs, nl, 32, first, err);
+  if (rc == 0 && Mz > 16)
+    rc = launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, fs, nl, 16, first, err);
+  if (rc == 0) rc = launch_band_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, fs, nl, 0, first, err);
+  fs.join();
   return rc;
 }
 

@@ -18,6 +18,7 @@
 #include <cstdio>
 
 #include "../../include/mpct.h"
+#include "launch_fan.h"
 #include "mpct_dev.h"
 
 namespace mpct {
@@ -30,12 +31,12 @@ long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
 // defined in mdband_kernel.hip
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
-                  hipStream_t stream, std::string* err);
+                  hipStream_t stream, LaunchFan* fan, std::string* err);
 long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu);
 // defined in nmpc_kernel.hip
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
-                std::string* err);
+                LaunchFan* fan, std::string* err);
 long long nmpc_lds_bytes(int M);
 }  // namespace mpct
 
@@ -88,6 +89,7 @@ struct mpct_scenario {
   DevScenario ds{};
   // scratch buffers for the host-pointer API (grow only)
   void* dscratch = nullptr;
+  LaunchFan fan;  // auxiliary streams of the class launches (band / NMPC kernels)
   size_t dscratch_bytes = 0;
 };
 
@@ -604,6 +606,7 @@ extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
     if (hipGetDevice(&cur) == hipSuccess && s->dev >= 0) (void)hipSetDevice(s->dev);
     if (s->dtab) (void)hipFree(s->dtab);
     if (s->dscratch) (void)hipFree(s->dscratch);
+    s->fan.release();
     if (cur >= 0) (void)hipSetDevice(cur);
   }
   delete s;
@@ -631,6 +634,15 @@ extern "C" int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, do
 }
 
 // ------------------------------------------------------------------------------------------
+// every per-lane history / coefficient set fits gpc_kernel.hip's register caps (kReg*)
+static int regpath(const mpct_scenario* s) {
+  bool rp = !s->mdband && !s->nmpc && s->pl_maxa - 1 <= kRegA;  // gpc_kernel.hip only
+  for (int e = 0; e < s->nvar * s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
+  for (int n = 0; rp && n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
+  for (int i = 0; rp && i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
+  return rp ? 1 : 0;
+}
+
 static int ensure_device(mpct_scenario* s, int want_dev) {
   int dev = want_dev;
   if (dev < 0) {
@@ -709,13 +721,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.ne = s->ne;
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
-  {
-    bool rp = !s->mdband && !s->nmpc && s->pl_maxa - 1 <= kRegA;  // gpc_kernel.hip only
-    for (int e = 0; e < s->nvar * s->ne; ++e) rp = rp && (s->pl_nb[e] - s->pl_off[e] <= kRegB);
-    for (int n = 0; rp && n < s->nu; ++n) rp = rp && (s->dum[n] <= kRegDu);
-    for (int i = 0; rp && i < s->my; ++i) rp = rp && (s->nyhi[i] <= kRegY);
-    ds.regpath = rp ? 1 : 0;
-  }
+  ds.regpath = regpath(s);
   ds.step = reinterpret_cast<const double*>(b + o_step);
   ds.phi = reinterpret_cast<const double*>(b + o_phi);
   ds.n1 = reinterpret_cast<const int*>(b + o_n1);
@@ -757,6 +763,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.nm = reinterpret_cast<const double*>(b + o_nm);
   s->dtab = dp;
   s->dev = dev;
+  if ((s->mdband || s->nmpc) && !s->fan.init(dev)) s->fan.release();  // no fan: one stream, still correct
   return MPCT_OK;
 }
 
@@ -802,9 +809,11 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
 #endif
   std::string err;
   if (s->nmpc)
-    rc = launch_nmpc(s->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, static_cast<hipStream_t>(stream), &err);
+    rc = launch_nmpc(s->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, static_cast<hipStream_t>(stream), &s->fan,
+                     &err);
   else if (s->mdband)
-    rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream), &err);
+    rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream),
+                       &s->fan, &err);
   else
     rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
                             static_cast<hipStream_t>(stream), &err);
@@ -927,5 +936,6 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.mz_maxa = s->mz_maxa;
   ds.fr_max = s->fr_max;
   ds.mdband = s->mdband;
+  ds.regpath = regpath(s);
   return s->mdband ? mdband_lds_bytes(ds, N2, Nu) : lds_bytes_for(ds, N2, Nu);
 }

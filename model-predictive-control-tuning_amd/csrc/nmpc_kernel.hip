@@ -23,6 +23,7 @@
 #include <math.h>
 
 #include "gi_core.h"
+#include "launch_fan.h"
 #include "mpct_dev.h"
 
 namespace mpct {
@@ -547,25 +548,30 @@ namespace mpct {
 
 long long nmpc_lds_bytes(int M) { return (long long)nm_layout(M).total * 8; }
 
-// one launch per QP size class (MAXM 16 / 32); a simulation runs in the launch of its class
+// one launch per QP size class (MAXM 16 / 32), the larger first, fanned over two streams so the
+// classes overlap (a simulation runs in the launch of its class; launch_fan.h)
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
-                std::string* err) {
+                LaunchFan* fan, std::string* err) {
   const int Mmax = sc.nu * sc.numax;
   if (Mmax > 32) {
     *err = "nu*nu_max > 32";
     return -4;
   }
-  {
-    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax);
-    hipLaunchKernelGGL(nmpc_closed_loop_kernel<16>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream,
-                       sc, C, nref, N, Nu, delta, lambda, r, o, out, 0);
-  }
+  FanScope fs(fan, stream);
+  int nl = 0;
   if (Mmax > 16) {
     const long long lds = nmpc_lds_bytes(Mmax);
-    hipLaunchKernelGGL(nmpc_closed_loop_kernel<32>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, stream,
-                       sc, C, nref, N, Nu, delta, lambda, r, o, out, 16);
+    hipLaunchKernelGGL(nmpc_closed_loop_kernel<32>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
+                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 16);
   }
+  {
+    // mz_lo == 0 marks the status-writing launch (padding / bad horizons)
+    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax);
+    hipLaunchKernelGGL(nmpc_closed_loop_kernel<16>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
+                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 0);
+  }
+  fs.join();
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     *err = std::string("kernel launch failed: ") + hipGetErrorString(e);

@@ -204,7 +204,9 @@ def _kernel_meta(text):
 def test_kernel_isa_invariants(built):
     """The single-wave LDS hand-offs (lds_sync = lgkmcnt(0)) require every helper inlined and no
     LDS access lowered to FLAT (a non-inlined gi_qp once raced this way at -O3).  The metric
-    size class (M <= 16) must also run without scratch and at 2 waves/SIMD (<= 256 VGPRs)."""
+    size class (M <= 16) runs at 3 waves/SIMD: <= 168 VGPRs (a few loop-invariant spills, 196 B of
+    scratch, measured 7 % faster than 2 waves/SIMD without them) and <= 160 KB / 12 of LDS at the
+    Shell 3x3 metric scenario."""
     import __graft_entry__ as g
 
     paths = g.kernel_isa()
@@ -216,4 +218,8 @@ def test_kernel_isa_invariants(built):
     assert "flat_load" not in text and "flat_store" not in text
     meta = _kernel_meta(text)
     assert set(meta) == {(m, d) for m in (16, 32, 64) for d in (0, 1)}   # (MAXM, DTC)
-    assert meta[(16, 0)]["scratch"] == 0 and meta[(16, 0)]["vgpr"] <= 256, meta[(16, 0)]
+    assert meta[(16, 0)]["scratch"] <= 256 and meta[(16, 0)]["vgpr"] <= 168, meta[(16, 0)]
+    from mpct.scenarios import shell3x3
+
+    sc, r, yref = shell3x3()
+    assert 12 * sc.lds_bytes(30, 5) <= 160 * 1024

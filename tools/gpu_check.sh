@@ -14,3 +14,8 @@ if [ "${CONFIG3:-1}" = "1" ]; then
     || { tail -20 "$O/config3.log"; exit 1; }
   tail -2 "$O/config3.log"
 fi
+if [ "${CONFIG5:-1}" = "1" ]; then
+  timeout -k 10 300 python3 tools/bench_config5.py --out "$O/config5.json" > "$O/config5.log" 2>&1 \
+    || { tail -20 "$O/config5.log"; exit 1; }
+  tail -1 "$O/config5.log"
+fi
