@@ -56,7 +56,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="thread-seconds of CPU baseline work")
+    ap.add_argument("--workload", default="shell3x3", choices=("shell3x3", "shell7x5", "vandevusse", "dtc-mc"),
+                    help="shell3x3 = the BASELINE metric (config 2); the others are SURVEY §8d configs 3, 5, 4")
     args = ap.parse_args()
+    if args.workload != "shell3x3":
+        return other_workload(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -216,6 +220,128 @@ def main():
         "top_candidate": int(order[0].item()),
     }
     print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def other_workload(args):
+    """SURVEY §8d configs 3-5 through the same harness (barrier + synchronize around K timed steps,
+    max over ranks, one JSON line on rank 0).  config 3 (shell7x5): the fixed 65,536-candidate
+    grid of tools/bench_config3.py split over the ranks (strong scaling, SURVEY: "65 536-candidate
+    grid sharded over 8xMI355X via RCCL"); config 5 (vandevusse): 4096 NMPC candidates per GPU;
+    config 4 (dtc-mc): 10,000 candidates x 32 plant-mismatch draws split over the ranks.  One
+    all-gather of the per-candidate cost records, identical ranking on every rank."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+
+        tdist.init_process_group("nccl", device_id=dev)
+    from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_range
+    from mpct.engine import eval_batch_device
+
+    v = None
+    nref = 1
+    if args.workload == "shell7x5":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_config3 import grid
+        from mpct.scenarios import SHELL7_W, shell7x5
+
+        sc, r, vv, _ = shell7x5(n2_max=127, nu_max=15)
+        N2, Nu, d, l = grid(1024)
+        refs, v = r[None], vv[None]
+        w = SHELL7_W
+        scaling, metric = "strong", "closed-loop band-MPC sims/sec (Shell 7x5, 65,536-candidate grid)"
+        cfg = {"workload": "Shell7x5 band-mode MPC, N2 x Nu x 1024 lambda grid, nit=200, sharded", "candidates": 65536}
+    elif args.workload == "vandevusse":
+        from mpct.nmpc import VDV_W, nmpc_candidate_grid, vandevusse
+
+        sc, r, _ = vandevusse()
+        N2, Nu, d, l = nmpc_candidate_grid(args.candidates * world)
+        refs = r[None]
+        w = VDV_W
+        scaling, metric = "weak", "closed-loop NMPC sims/sec (Van de Vusse, Gauss-Newton SQP)"
+        cfg = {"workload": "VanDeVusse NMPC, N in 3..31, Nu in 2..15, nit=60 + open loop",
+               "candidates_per_gpu": args.candidates}
+    else:
+        from mpct.dtc import woodberry_mc
+
+        D = 32
+        sc, r, vv, _ = woodberry_mc(draws=D, n2_max=30, nu_max=10)
+        rng = np.random.default_rng(20250307)
+        Cc = 10000
+        N2 = rng.integers(3, 31, Cc).astype(np.int32)
+        Nu = np.array([rng.integers(1, min(p, 10) + 1) for p in N2], dtype=np.int32)
+        l = 10.0 ** rng.uniform(-3, 1, (Cc, 2))
+        d = 10.0 ** rng.uniform(-3, 1, (Cc, 2))
+        refs, v, nref = r, vv, D
+        w = np.ones(2)
+        scaling, metric = "strong", "closed-loop DTC-GPC sims/sec (WoodBerry, 10,000 candidates x 32 draws)"
+        cfg = {"workload": "WoodBerry DTC-GPC Monte-Carlo, nit=200, sharded by candidate", "candidates": Cc,
+               "draws": D}
+    Cg = len(N2)
+    lo, hi = shard_range(Cg, world, rank)
+    sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, lo, hi)
+    C = hi - lo
+    S = C * nref
+    t = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in
+         dict(N2=sN2, Nu=sNu, d=sd, l=sl, r=refs).items()}
+    tv = torch.from_numpy(np.ascontiguousarray(v)).to(dev) if v is not None else None
+    out = dict(J1=torch.empty((S, sc.my), dtype=torch.float64, device=dev),
+               status=torch.empty(S, dtype=torch.int32, device=dev),
+               qp_iters=torch.empty(S, dtype=torch.int64, device=dev))
+    tw = torch.tensor(w, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    kev = []
+
+    def step(record):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eval_batch_device(sc, t["N2"], t["Nu"], t["d"], t["l"], t["r"], out, v=tv, device=local, stream=stream)
+        e1.record(stream)
+        if record:
+            kev.append((e0, e1))
+        J = out["J1"].view(C, nref, sc.my).amax(dim=1) if nref > 1 else out["J1"]  # worst case over draws
+        costs = gather_costs(J) if dist else J
+        return rank_candidates(costs, tw, Cg)
+
+    steps = args.steps if args.steps != 20 else 2   # a step is a whole grid here (seconds)
+    warm = args.warmup if args.warmup != 3 else 1
+    for _ in range(warm):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        order = step(True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(te, op=tdist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+    st = out["status"].cpu().numpy()
+    if rank == 0:
+        sims = (Cg * nref if scaling == "strong" else world * S) * steps
+        line = {"metric": metric, "value": sims / elapsed, "unit": "sims/s", "n_gpus": world, "steps": steps,
+                "warmup": warm, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": scaling,
+                "vs_baseline": None, "dtype": "f64", "data": "synthetic candidate grid (seed 20250307) on the "
+                "reference's scenario", "config": dict(cfg, parallelism="dp%d" % world),
+                "roofline": None, "kernel_ms_rank0": kms, "cpu_baseline": None,
+                "status_codes": {int(k): int(n) for k, n in zip(*np.unique(st, return_counts=True))},
+                "top_candidate": int(order[0].item())}
+        print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
 

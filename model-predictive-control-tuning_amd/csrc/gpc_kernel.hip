@@ -27,6 +27,12 @@
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // 168 VGPRs: 3 waves per SIMD, which the trimmed LDS (13.4 KB at Shell 3x3) allows
 #endif
+#ifndef MPCT_REG_DU
+#define MPCT_REG_DU 0  // past-control registers in VGPRs (else shifted in LDS; 0 measured faster)
+#endif
+#ifndef MPCT_REG_Y
+#define MPCT_REG_Y 0   // y backward-difference histories in VGPRs (else in LDS; 0 measured faster)
+#endif
 namespace mpct {
 
 struct LdsLayout {
@@ -360,24 +366,6 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
     }
   }
   for (int e = lane; e < L.plb - L.x; e += kWave) lds[L.x + e] = 0.0;  // state + histories
-  // per-lane constants in registers
-  const int yoff_i = lane < my ? sc.yoff[lane] : 0;
-  const int nyh_i = lane < my ? sc.nyhi[lane] : 0;
-  const int upoff_n = lane < nu ? sc.upoff[lane] : 0;
-  const int dum_n = lane < nu ? sc.dum[lane] : 0;
-  RowCons rcn;
-  rcn.n = lane < M ? lane / Nu : 0;
-  rcn.l = lane < M ? lane - rcn.n * Nu : 0;
-  rcn.dmin = sc.bnd[rcn.n];
-  rcn.dmax = sc.bnd[nu + rcn.n];
-  rcn.umin = sc.bnd[2 * nu + rcn.n];
-  rcn.umax = sc.bnd[3 * nu + rcn.n];
-  const int ecopy = lane / ne;
-  const int ee = lane - ecopy * ne;
-  const int ej = ee % nin;
-  const int e_nb = (lane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
-  const int e_na = (lane < ne * 2) ? sc.pl_na[pve + ee] : 0;
-  const int e_off = (lane < ne * 2) ? sc.pl_off[pve + ee] : 0;
   const double* dl = deltav + c * my;
   const double* lm = lambdav + c * nu;
   lds_sync();
@@ -507,6 +495,25 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
   return;
 #endif
 
+  // per-lane constants of the step loop, defined after the prologue so that they are not live
+  // (and spilled) across its register-heavy QR
+  const int yoff_i = lane < my ? sc.yoff[lane] : 0;
+  const int nyh_i = lane < my ? sc.nyhi[lane] : 0;
+  const int upoff_n = lane < nu ? sc.upoff[lane] : 0;
+  const int dum_n = lane < nu ? sc.dum[lane] : 0;
+  RowCons rcn;
+  rcn.n = lane < M ? lane / Nu : 0;
+  rcn.l = lane < M ? lane - rcn.n * Nu : 0;
+  rcn.dmin = sc.bnd[rcn.n];
+  rcn.dmax = sc.bnd[nu + rcn.n];
+  rcn.umin = sc.bnd[2 * nu + rcn.n];
+  rcn.umax = sc.bnd[3 * nu + rcn.n];
+  const int ecopy = lane / ne;
+  const int ee = lane - ecopy * ne;
+  const int ej = ee % nin;
+  const int e_nb = (lane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
+  const int e_na = (lane < ne * 2) ? sc.pl_na[pve + ee] : 0;
+  const int e_off = (lane < ne * 2) ? sc.pl_off[pve + ee] : 0;
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 8 * M + 16;
   long long iters = 0;
@@ -717,7 +724,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
         ym = ygz + yfr;
       }
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
-      if (regpath) {  // yd = [y(t-1), nabla y(t-1), ...] in registers
+      if (regpath && MPCT_REG_Y) {  // yd = [y(t-1), nabla y(t-1), ...] in registers
         double cur = ym, prev = yd[0];
 #pragma unroll
         for (int k = 1; k < kRegY; ++k) {
@@ -762,7 +769,7 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
-      if (regpath) {  // past-control register in registers, written out whole
+      if (regpath && MPCT_REG_DU) {  // past-control register in registers, written out whole
 #pragma unroll
         for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
         duh[0] = du;
