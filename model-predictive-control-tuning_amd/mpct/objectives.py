@@ -34,15 +34,27 @@ def gam_fun(sc, X, N, Nu, Xsp, ov_weights=None):
     return res.J1, res
 
 
-def vns_objective(sc, N2, Nu, delta, lam, inK=10, device=-1):
+def vns_refs_nonlinear(Xsp):
+    """Nonlinear models keep the driver's setpoint Par.Xsp (VNS2.m:67-71 leaves it as is) and
+    simulate Xsp.*sel, one output selected at a time (VNS2.m:148-155): the unselected outputs get
+    a zero reference, as in the reference."""
+    Xsp = np.asarray(Xsp, dtype=float)
+    my = Xsp.shape[0]
+    return np.stack([Xsp * (np.arange(my) == i)[:, None] for i in range(my)])
+
+
+def vns_objective(sc, N2, Nu, delta, lam, inK=10, device=-1, refs=None):
     """F = sum(j21 + j22) + N(1) + sum(Jnu) (VNS2.m:195) for C candidates (square plant: my
     simulations per candidate, output i / MV i taken from simulation i, VNS2.m:148-165).
+    refs: the my reference sets (default: the linear models' unit steps at inK, VNS2.m:58-61;
+    vns_refs_nonlinear for an NMPC scenario).
     Returns (F (C,), j21 (C,my), j22 (C,my), Jnu (C,nu), EvalResult)."""
     if sc.my != sc.nu:
         raise NotImplementedError("non-square VNS path (VNS2.m:168) is a later-round item")
     N2 = np.atleast_1d(N2).astype(np.int32)
     Cn = N2.size
-    refs = vns_step_refs(sc.my, sc.nit, inK)
+    if refs is None:
+        refs = vns_step_refs(sc.my, sc.nit, inK)
     res = eval_batch(sc, N2, Nu, delta, lam, refs, open_loop=True, device=device)
     idx = np.arange(sc.my)
     j21 = res.j21.reshape(Cn, sc.my, sc.my)[:, idx, idx]

@@ -368,7 +368,7 @@ def save_tuning_parameters(path: str, N, Nu, delta, lam, scale: dict | None = No
 
 
 # --------------------------------------------------------------------------------------------
-def engine_evaluators(sc, r, par: TuningPar, device: int = -1):
+def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None):
     """Batched evaluators over the HIP engine (one eval_batch call per batch):
       batch_j1(X rows)                 -> J1 rows  (GAM_fun.m:55-116 with Par.N / Par.Nu, which
                                           closedloop_toolbox reduces with max, :36-40)
@@ -399,7 +399,7 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1):
         Nu = np.array([max(k[1]) for k in keys], dtype=np.int32)
         d = np.tile(np.asarray(delta, dtype=float), (C, 1))
         l = np.tile(np.asarray(lam, dtype=float), (C, 1))
-        F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device)
+        F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device, refs=vns_refs)
         ok = res.status.reshape(C, -1).max(axis=1) == 0
         return np.where(ok, F, np.nan)
 
@@ -408,15 +408,22 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1):
 
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
-               gam_max_iter: int = 400):
+               gam_max_iter: int = 400, lineal: bool = True):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
-    (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters."""
+    (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
+    lineal = False: a nonlinear (NMPC) scenario (MPCTuning.m:202-250): VNS simulates the driver's
+    setpoint one output at a time instead of unit steps (VNS2.m:67-71,148-155)."""
     par = TuningPar(my=my, ny=ny, nbp=nbp, nbc=nbc, dmin=dmin, w=w, q0=q0, w0=w0, nit=sc.nit)
     if sc.n2_max < 2 ** par.nbp - 1 or sc.nu_max < 2 ** par.nbc - 1:
         raise ValueError("scenario horizons (n2_max=%d, nu_max=%d) must cover the bit ranges "
                          "(%d, %d)" % (sc.n2_max, sc.nu_max, 2 ** par.nbp - 1, 2 ** par.nbc - 1))
-    batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device)
+    vns_refs = None
+    if not lineal:
+        from .objectives import vns_refs_nonlinear
+
+        vns_refs = vns_refs_nonlinear(r)
+    batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device, vns_refs=vns_refs)
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
                                                   gam_max_iter=gam_max_iter)
     if save_path:
