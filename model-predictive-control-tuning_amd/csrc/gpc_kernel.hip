@@ -142,11 +142,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
     double s[4];
     slacks(xu, s);
     const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
-    if (__ballot(smin < -tol) == 0) {
-      if (row) sxc[lane] = xu;
-      lds_sync();
-      return 0;
-    }
+    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
     if (S.q == 0) {
       S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
     } else {

@@ -288,3 +288,23 @@ def test_band_config3_grid_hard_cases(gpu):
         one = _run(sc, [c], r, v, open_loop=False)
         np.testing.assert_array_equal(one.u[0], res.u[k])
         np.testing.assert_array_equal(one.J1[0], res.J1[k])
+
+
+@pytest.mark.gpu
+def test_band_statuses_in_mixed_batch(gpu):
+    """Padding and bad horizons are reported once (by the first class launch) in a batch that
+    spans every (QP size, LDS) class; the valid candidates' results are those of single runs."""
+    from mpct.scenarios import shell7x5
+
+    sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
+    cands = [(0, 1), (16, 2), (127, 15), (20, 30), (10, 12), (64, 8), (200, 2)]
+    lam = np.array([0.05, 0.02, 1.6])
+    N2 = np.array([c[0] for c in cands], np.int32)
+    Nu = np.array([c[1] for c in cands], np.int32)
+    from mpct.engine import eval_batch
+
+    res = eval_batch(sc, N2, Nu, np.zeros((7, 7)), np.tile(lam, (7, 1)), r[None], v=v[None])
+    assert res.status.tolist() == [8, 0, 0, 16, 16, 0, 16], res.status
+    for k in (1, 2, 5):
+        one = eval_batch(sc, N2[k:k + 1], Nu[k:k + 1], np.zeros((1, 7)), lam[None], r[None], v=v[None])
+        np.testing.assert_array_equal(one.J1[0], res.J1[k])

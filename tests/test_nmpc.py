@@ -167,3 +167,52 @@ def test_nmpc_gpu_deterministic_and_order_free(gpu):
     b = eval_batch(sc, N[::-1], Nu[::-1], d[::-1], lam[::-1], r[None])
     np.testing.assert_array_equal(a.J1, b.J1[::-1])
     assert np.mean(a.status == 0) > 0.95, np.unique(a.status, return_counts=True)
+
+
+@pytest.mark.gpu
+def test_nmpc_gpu_vns_references_and_statuses(gpu):
+    """VNS on a nonlinear model simulates Xsp.*sel per output (VNS2.m:148-155): two reference
+    sets per candidate ride on the reference dimension, each equal to the oracle's loop on that
+    reference; padding (N = 0) and bad horizons (Nu > N, N > n_max) come back as status 8 / 16
+    with NaN costs; an empty batch is a no-op."""
+    import oracle.nmpc_vdv as nv
+    from mpct.engine import eval_batch
+    from mpct.nmpc import nmpc_candidate_grid, vandevusse
+    from mpct.objectives import vns_refs_nonlinear
+
+    sc, r, yref = vandevusse()
+    refs = vns_refs_nonlinear(r)
+    N, Nu, d, lam = nmpc_candidate_grid(64)
+    pick = [0, 4]
+    res = eval_batch(sc, N[pick], Nu[pick], d[pick], lam[pick], refs, open_loop=True, want_traj=True)
+    assert res.y.shape[0] == 4
+    ncmp = 0
+    for ci, k in enumerate(pick):
+        for j in range(2):
+            its = []
+            orig = nv.controller
+
+            def spy(*a, _o=orig):
+                U, it = _o(*a)
+                its.append(it)
+                return U, it
+
+            nv.controller = spy
+            try:
+                o = nv.closedloop_nmpc(refs[j], int(N[k]), int(Nu[k]), d[k], lam[k])
+            finally:
+                nv.controller = orig
+            s = ci * 2 + j
+            # a controller call that stops at the iteration cap is path dependent (Armijo decisions
+            # at rounding-level ties): both sides must report it, and only converged loops compare
+            assert bool(res.status[s] & 32) == (max(its) >= nv.SQP_MAX), (k, j, res.status[s], max(its))
+            if res.status[s] & 32:
+                continue
+            ncmp += 1
+            assert _trel(res.y[s], o.y) < TRAJ_RTOL and _trel(res.uopt[s], o.uopt) < TRAJ_RTOL, (k, j)
+    assert ncmp >= 2
+    bad = eval_batch(sc, [0, 5, 40, 6], [2, 6, 2, 3], np.ones((4, 2)), np.ones((4, 2)) * 0.1, r[None])
+    assert bad.status.tolist()[:3] == [8, 16, 16] and bad.status[3] & 31 == 0
+    assert np.all(np.isnan(bad.J1[:3])) and np.all(np.isfinite(bad.J1[3]))
+    empty = eval_batch(sc, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 2)), np.zeros((0, 2)), r[None])
+    assert empty.J1.shape == (0, 2)
