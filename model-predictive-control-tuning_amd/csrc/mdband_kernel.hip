@@ -38,36 +38,39 @@ struct BandLayout {
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
-// LDS copy of the MV step table: samples 0..N2 (+1 spare) of each entry, row stride tls
-__host__ __device__ inline int band_tls(const DevScenario& sc, int N2) { return sc.tlen < N2 + 2 ? sc.tlen : N2 + 2; }
+// LDS copy of the MV step table: samples 0..N2 of each entry, row stride tls
+__host__ __device__ inline int band_tls(const DevScenario& sc, int N2) { return sc.tlen < N2 + 1 ? sc.tlen : N2 + 1; }
 
-__host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2, int M) {
+// full_ri: R^-1 is a full triangle (some OV weight > 0); in band mode R is diagonal and only its
+// inverse diagonal is kept.  ncopy: 2 with the open-loop prediction (a second plant copy), else 1
+__host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2, int M, bool full_ri = true,
+                                                  int ncopy = 2) {
   const int Mz = M + 1, my = sc.my, nu = sc.nu, nin = sc.nin, ne = sc.ne;
   BandLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
-  L.ri = take(Mz * Mz);
+  L.ri = take(full_ri ? Mz * Mz : Mz);
   L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
   L.ra = take(Mz * Mz);  // R_A
   L.dv = take(Mz);       // d = J'n
   L.nv = take(Mz);       // staged normal n_p
   L.xc = take(Mz);       // QP iterate
-  L.gv = take(Mz);       // linear term / triangular-solve scratch
+  L.gv = take(full_ri ? Mz : 0);  // linear term / triangular-solve scratch (tracking weights only)
   L.sl = take(4 * Mz);   // box slacks at the unconstrained minimiser
   L.ob = take(4 * my);   // y_min, y_max, V_min s_y, V_max s_y
   L.fr = take(2 * my * N2);                // free-response window, double-buffered by t parity
   L.bits = take((2 * my * N2 + 63) / 64);  // active output rows (32-bit words)
   L.du = take(nu);                         // du(t-1)
   L.uprev = take(nu);
-  L.ucum = take(M);
-  L.ye = take(2 * ne);
-  L.yeh = take(2 * ne * kYeHist);
-  L.uring = take(2 * nin * kURing);
+  L.ucum = take(ncopy == 2 ? M : 0);  // open-loop Uopt only
+  L.ye = take(ncopy * ne);
+  L.yeh = take(ncopy * ne * kYeHist);
+  L.uring = take(ncopy * nin * kURing);
   L.tail = take(ne * kYeHist);  // model entry tails of the window
   L.sext = take(ne);            // model entry window extensions
-  L.plb = take(ne * sc.pl_maxb);
+  L.plb = take(ne * sc.pl_maxbc);  // compact: taps from the first nonzero one
   L.pla = take(ne * sc.pl_maxa);
-  L.mzb = take(ne * sc.mz_maxb);
+  L.mzb = take(ne * sc.mz_maxbc);
   L.mza = take(ne * sc.mz_maxa);
   L.step = take(my * nu * band_tls(sc, N2));
   L.total = (o + 1) & ~1;
@@ -129,7 +132,16 @@ __global__ void __launch_bounds__(64, 1)
     if (first) write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
-  const BandLayout L = band_layout(sc, N2, M);
+  const double* dl = deltav + c * my;
+  const double* lm = lambdav + c * nu;
+  // toolbox weights over scale factors: q_i = (delta_i / s_y,i)^2, w_n = (lambda_n / s_u,n)^2
+  auto qw = [&](int i) __attribute__((always_inline)) -> double {
+    const double w = fabs(dl[i]) * sc.wscale[i];
+    return sc.wsq ? w * w : w;
+  };
+  bool any_q = false;  // some OV tracked: R full; band mode: R (and J = R^-1) diagonal
+  for (int i = 0; i < my; ++i) any_q = any_q || qw(i) > 0.0;
+  const BandLayout L = band_layout(sc, N2, M, any_q, o.open_loop ? 2 : 1);
   // this launch serves one (QP size, LDS) class: the others' simulations leave at once
   if (Mz <= mz_lo || Mz > MAXM || (long long)L.total * 8 <= lds_lo || (long long)L.total * 8 > lds_hi) return;
   const int tls = band_tls(sc, N2);
@@ -163,9 +175,15 @@ __global__ void __launch_bounds__(64, 1)
     const int en = e / tls;
     sstep[e] = sc.step[en * tlen + (e - en * tls)];
   }
-  for (int e = lane; e < ne * sc.pl_maxb; e += kWave) splb[e] = sc.pl_b[e];
+  for (int e = lane; e < ne * sc.pl_maxbc; e += kWave) {
+    const int en = e / sc.pl_maxbc, l = e - en * sc.pl_maxbc, off = sc.pl_off[en];
+    splb[e] = off + l < sc.pl_nb[en] ? sc.pl_b[en * sc.pl_maxb + off + l] : 0.0;
+  }
   for (int e = lane; e < ne * sc.pl_maxa; e += kWave) spla[e] = sc.pl_a[e];
-  for (int e = lane; e < ne * sc.mz_maxb; e += kWave) smzb[e] = sc.mz_b[e];
+  for (int e = lane; e < ne * sc.mz_maxbc; e += kWave) {
+    const int en = e / sc.mz_maxbc, l = e - en * sc.mz_maxbc, off = sc.mz_off[en];
+    smzb[e] = off + l < sc.mz_nb[en] ? sc.mz_b[en * sc.mz_maxb + off + l] : 0.0;
+  }
   for (int e = lane; e < ne * sc.mz_maxa; e += kWave) smza[e] = sc.mz_a[e];
   for (int e = lane; e < 4 * my; e += kWave) sob[e] = sc.obnd[e];
   for (int e = lane; e < L.plb - L.fr; e += kWave) lds[L.fr + e] = 0.0;
@@ -177,13 +195,6 @@ __global__ void __launch_bounds__(64, 1)
   rcn.dmax = sc.bnd[nu + rcn.n];
   rcn.umin = sc.bnd[2 * nu + rcn.n];
   rcn.umax = sc.bnd[3 * nu + rcn.n];
-  const double* dl = deltav + c * my;
-  const double* lm = lambdav + c * nu;
-  // toolbox weights over scale factors: q_i = (delta_i / s_y,i)^2, w_n = (lambda_n / s_u,n)^2
-  auto qw = [&](int i) __attribute__((always_inline)) -> double {
-    const double w = fabs(dl[i]) * sc.wscale[i];
-    return sc.wsq ? w * w : w;
-  };
   lds_sync();
 
   // QR of W = [Q^1/2 G (outputs with q_i > 0); Lambda^1/2; rho^1/2 e_eps] by row-streamed Givens
@@ -240,8 +251,11 @@ __global__ void __launch_bounds__(64, 1)
       write_nan(MPCT_ST_NONFINITE_);
       return;
     }
-    // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
-    if (row) {
+    // R^-1 (upper, row-major): lane j solves R x = e_j in its own column; band mode: R is
+    // diagonal, only 1/R_jj is kept
+    if (row && !any_q) {
+      sRi[lane] = 1.0 / sR[lane * Mz + lane];
+    } else if (row) {
       for (int kk = lane; kk >= 0; --kk) {
         double a = (kk == lane) ? 1.0 : 0.0;
         for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * Mz + j] * sRi[j * Mz + lane];
@@ -251,8 +265,6 @@ __global__ void __launch_bounds__(64, 1)
     }
     lds_sync();
   }
-  bool any_q = false;
-  for (int i = 0; i < my; ++i) any_q = any_q || qw(i) > 0.0;
 
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 200 * Mz + 1000;
@@ -267,6 +279,20 @@ __global__ void __launch_bounds__(64, 1)
   int dbg_t = -1;
 #endif
 
+  // J = R^-1 (gi_load_rinv), or its diagonal in band mode
+  auto load_j = [&]() __attribute__((always_inline)) {
+    if (any_q) {
+      gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+    } else {
+      if (row) {
+        const double dj = sRi[lane];
+        for (int k = 0; k < Mz; ++k) sJT[k * Mz + lane] = k == lane ? dj : 0.0;
+      }
+      gis.nrot = 0;
+      gis.jinit = true;
+      lds_sync();
+    }
+  };
   // predicted output of row g = i*N2 + k at the iterate in sxc: F[g] + G_g dU
   auto yhat = [&](const double* F, int g) __attribute__((always_inline)) -> double {
     const int i = g / N2, k = g - i * N2;
@@ -436,7 +462,7 @@ __global__ void __launch_bounds__(64, 1)
       lds_sync();
       if (force || !gis.jinit || gis.nrot >= 4 * Mz) {
         const int qq = gis.q;
-        gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+        load_j();
         gis.q = 0;
         for (int v = 0; v < qq; ++v) {
           const int p = __builtin_amdgcn_readlane(gis.ww, v);
@@ -530,7 +556,7 @@ __global__ void __launch_bounds__(64, 1)
         xm = recentre(true);
         continue;
       }
-      if (!gis.jinit) gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+      if (!gis.jinit) load_j();
       const int p = bid;
       double sp = best, upm = 0.0;
       bool infeas = false;
@@ -642,7 +668,7 @@ __global__ void __launch_bounds__(64, 1)
     // plant entries y_e(t) (copy 0 closed loop, copy 1 open loop driven by uopt)
     for (int e = lane; e < ncopy * ne; e += kWave) {
       const int cpy = e / ne, ee = e - cpy * ne, j = ee % nin;
-      const double* eb = splb + ee * sc.pl_maxb;
+      const double* eb = splb + ee * sc.pl_maxbc - sc.pl_off[ee];  // tap l at eb[l], l >= off
       const double* ea = spla + ee * sc.pl_maxa;
       const double* eur = sur + (cpy * nin + j) * kURing;
       double* eyh = syeh + e * kYeHist;
@@ -677,7 +703,7 @@ __global__ void __launch_bounds__(64, 1)
     // step at tau = t + N2 (MVs u(min(tau', t-1)), MDs v(min(tau', t)))
     for (int e = lane; e < ne; e += kWave) {
       const int i = e / nin, j = e - i * nin;
-      const double* mb = smzb + e * sc.mz_maxb;
+      const double* mb = smzb + e * sc.mz_maxbc - sc.mz_off[e];  // tap l at mb[l], l >= off
       const double* ma = smza + e * sc.mz_maxa;
       const double* eur = sur + j * kURing;
       double* tl = stail + e * kYeHist;
@@ -795,8 +821,8 @@ __global__ void __launch_bounds__(64, 1)
 
 namespace mpct {
 
-long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu) {
-  const BandLayout L = band_layout(sc, N2, sc.nu * Nu);
+long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy) {
+  const BandLayout L = band_layout(sc, N2, sc.nu * Nu, true, ncopy);
   return (long long)L.total * 8;
 }
 
@@ -815,7 +841,7 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
                          std::string* err) {
   const int nu_hi = std::min(sc.numax, (MAXM - 1) / sc.nu);
   if (nu_hi < 1) return 0;
-  const long long lds_max = mdband_lds_bytes(sc, sc.n2max, nu_hi);
+  const long long lds_max = mdband_lds_bytes(sc, sc.n2max, nu_hi, o.open_loop ? 2 : 1);
   if (lds_max > 160 * 1024) {
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;

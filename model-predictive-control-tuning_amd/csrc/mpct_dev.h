@@ -76,6 +76,7 @@ struct DevScenario {
   const double* step_md;  // [my][nd][tlen]  model MD step responses
   const double* obnd;     // [4][my]  y_min, y_max, MinECR*s_y, MaxECR*s_y (+-inf: no bound)
   const double* wscale;   // [my + nu]  1/s_y, 1/s_u (weights over ScaleFactors)
+  int pl_maxbc, mz_maxbc; // longest run of numerator taps from the first nonzero one (compact LDS copies)
   // nonlinear MPC (nmpc = 1, nmpc_kernel.hip): my = outputs, nu = MVs, n2max = largest N
   int nmpc;
   int nsub, sqp_max;

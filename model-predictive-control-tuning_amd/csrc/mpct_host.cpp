@@ -32,7 +32,7 @@ long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
                   hipStream_t stream, LaunchFan* fan, std::string* err);
-long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu);
+long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy);
 // defined in nmpc_kernel.hip
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
@@ -643,6 +643,16 @@ static int regpath(const mpct_scenario* s) {
   return rp ? 1 : 0;
 }
 
+// longest run of numerator taps from each entry's first nonzero one (mdband_kernel.hip keeps only
+// those in LDS: the delay's leading zeros are skipped by pl_off / mz_off anyway)
+static void compact_taps(const mpct_scenario* s, DevScenario& ds) {
+  int pb = 1, mb = 1;
+  for (size_t e = 0; e < s->pl_nb.size(); ++e) pb = std::max(pb, s->pl_nb[e] - s->pl_off[e]);
+  for (size_t e = 0; e < s->mz_nb.size(); ++e) mb = std::max(mb, s->mz_nb[e] - s->mz_off[e]);
+  ds.pl_maxbc = pb;
+  ds.mz_maxbc = mb;
+}
+
 static int ensure_device(mpct_scenario* s, int want_dev) {
   int dev = want_dev;
   if (dev < 0) {
@@ -754,6 +764,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.step_md = reinterpret_cast<const double*>(b + o_smd);
   ds.obnd = reinterpret_cast<const double*>(b + o_obnd);
   ds.wscale = reinterpret_cast<const double*>(b + o_wsc);
+  compact_taps(s, ds);
   ds.nmpc = s->nmpc;
   ds.nsub = s->nsub;
   ds.sqp_max = s->sqp_max;
@@ -937,5 +948,8 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.fr_max = s->fr_max;
   ds.mdband = s->mdband;
   ds.regpath = regpath(s);
-  return s->mdband ? mdband_lds_bytes(ds, N2, Nu) : lds_bytes_for(ds, N2, Nu);
+  ds.my = s->my;
+  ds.nd = s->nd;
+  compact_taps(s, ds);
+  return s->mdband ? mdband_lds_bytes(ds, N2, Nu, 2) : lds_bytes_for(ds, N2, Nu);
 }
