@@ -59,8 +59,9 @@ __device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const d
   const double ca = x[0], cb = x[1], T = x[2];
   const double th = T + 273.15;
   const double ith = 1.0 / th;
-  const double k1 = P.k10 * exp(P.e1 * ith);
-  const double k2 = P.k20 * exp(P.e2 * ith);
+  const double ex1 = exp(P.e1 * ith);
+  const double k1 = P.k10 * ex1;
+  const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp(P.e2 * ith));  // E1 = E2 in the reference model
   const double k3 = P.k30 * exp(P.e3 * ith);
   const double fov = u[0], tk = u[1];
   f[0] = fov * (P.ca0 - ca) - k1 * ca - k3 * ca * ca;
