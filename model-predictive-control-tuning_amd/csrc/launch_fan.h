@@ -52,14 +52,15 @@ struct FanScope {
   hipStream_t main;
   bool used[kFanAux] = {};
   bool forked = false;
-  FanScope(LaunchFan* f, hipStream_t s) : fan(f && f->ready ? f : nullptr), main(s) {}
+  // the fork point is recorded before any class launch: an auxiliary stream must not wait for a
+  // class launch already queued on the caller's stream
+  FanScope(LaunchFan* f, hipStream_t s) : fan(f && f->ready ? f : nullptr), main(s) {
+    if (fan) forked = hipEventRecord(fan->fork, main) == hipSuccess;
+    if (!forked) fan = nullptr;
+  }
   hipStream_t stream(int k) {
     if (!fan || k % (kFanAux + 1) == 0) return main;
     const int a = k % (kFanAux + 1) - 1;
-    if (!forked) {
-      (void)hipEventRecord(fan->fork, main);
-      forked = true;
-    }
     if (!used[a]) {
       (void)hipStreamWaitEvent(fan->aux[a], fan->fork, 0);
       used[a] = true;
