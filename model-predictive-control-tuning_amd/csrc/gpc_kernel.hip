@@ -25,7 +25,8 @@
 #include "gi_core.h"
 
 #ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 3  // 168 VGPRs: 3 waves per SIMD, which the trimmed LDS (13.4 KB at Shell 3x3) allows
+#define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
+                             // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
 #endif
 #ifndef MPCT_REG_DU
 #define MPCT_REG_DU 0  // past-control registers in VGPRs (else shifted in LDS; 0 measured faster)
@@ -290,7 +291,7 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
 
 
 template <int MAXM, bool DTC>
-__global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
+__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
                            const double* __restrict__ deltav, const double* __restrict__ lambdav,
@@ -820,7 +821,8 @@ __global__ void __launch_bounds__(64, MPCT_WAVES_PER_EU)
 #include <string>
 
 #ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 3  // 168 VGPRs: 3 waves per SIMD, which the trimmed LDS (13.4 KB at Shell 3x3) allows
+#define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
+                             // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
 #endif
 namespace mpct {
 
