@@ -290,7 +290,9 @@ __device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& 
 }
 
 
-template <int MAXM, bool DTC>
+// EXT: the open-loop prediction and/or trajectories may be requested; the EXT = false instance
+// (GAM scoring: costs only) carries none of their state through the step loop
+template <int MAXM, bool DTC, bool EXT>
 __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
@@ -576,7 +578,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
 
   // ------------------------------------------------------------------ open-loop prediction
   double jnu = 0.0;
-  if (o.open_loop) {
+  if ((EXT && o.open_loop)) {
     // closedloop_toolbox.m:86-91: initial state (y = 0), reference r(:, end)
     if (lane < my) sx[yoff_i] = -rr[lane * nit + (nit - 1)];
     lds_sync();
@@ -604,7 +606,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
 
   // ------------------------------------------------------------------ closed loop
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
-  const int ncopy = o.open_loop ? 2 : 1;
+  const int ncopy = (EXT && o.open_loop) ? 2 : 1;
   const bool is_entry = lane < ncopy * ne;
   const double* eb = splb + ee * sc.pl_maxb;
   const double* ea = spla + ee * sc.pl_maxa;
@@ -632,6 +634,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     yr_t = sc.yref[lane * nit];
   }
   for (int t = 0; t < nit; ++t) {
+    // the lane predicates of the step are re-derived from an opaque copy of the lane id every
+    // step: hoisted out of the loop they are kept as SGPR-pair exec masks, which the kernel's
+    // SGPR budget spills to VGPR lanes and reloads (v_readlane) several times per step
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     double r_n = 0.0, yr_n = 0.0;
     if (lane < my && t + 1 < nit) {  // prefetch t+1
       r_n = rr[lane * nit + t + 1];
@@ -644,13 +651,13 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
         sur[(cpy * nin + nu + j) * kURing + (t & (kURing - 1))] = vvk[j * nit + t];
       }
     }
-    if (o.open_loop && lane < nu) {
+    if ((EXT && o.open_loop) && lane < nu) {
       const int l = t < Nu - 1 ? t : Nu - 1;
       sur[(nin + lane) * kURing + (t & (kURing - 1))] = sucum[lane * Nu + l];
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    if (is_entry) {
+    if (ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double acc;
@@ -695,7 +702,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
       }
       lds_sync();
     }
-    if (lane < my) {
+    if (ln < my) {
       const int i = lane;
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
@@ -750,19 +757,19 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
       j1 += e1 * e1;
       if (t >= sc.ink0) j22 += e1 * e1;
       double ysv = 0.0;
-      if (o.open_loop) {
+      if ((EXT && o.open_loop)) {
         for (int j = 0; j < nin; ++j) ysv += sye[ne + i * nin + j];
         if (t >= sc.ink0) j21 += (y - ysv) * (y - ysv);
       }
-      if (o.want_traj) {
+      if ((EXT && o.want_traj)) {
         if (out.y) out.y[(sim * my + i) * nit + t] = y;
-        if (o.open_loop && out.ys) out.ys[(sim * my + i) * nit + t] = ysv;
+        if ((EXT && o.open_loop) && out.ys) out.ys[(sim * my + i) * nit + t] = ysv;
       }
     }
     lds_sync();
     PSTAMP(PROF_YUPD);
     solve_step();
-    if (lane < nu) {
+    if (ln < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
@@ -778,9 +785,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
         sx[upoff_n] = du;
       }
       sur[n * kURing + (t & (kURing - 1))] = un;
-      if (o.want_traj) {
+      if ((EXT && o.want_traj)) {
         if (out.u) out.u[(sim * nu + n) * nit + t] = un;
-        if (o.open_loop && out.uopt) {
+        if ((EXT && o.open_loop) && out.uopt) {
           const int l = t < Nu - 1 ? t : Nu - 1;
           // Info.Uopt has p+1 rows then the padding repeats the last row (:94-98)
           out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
@@ -803,9 +810,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;
     if (out.J1) out.J1[sim * my + lane] = j1;
     if (out.j22) out.j22[sim * my + lane] = j22;
-    if (out.j21) out.j21[sim * my + lane] = o.open_loop ? j21 : NAN;
+    if (out.j21) out.j21[sim * my + lane] = (EXT && o.open_loop) ? j21 : NAN;
   }
-  if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = o.open_loop ? jnu : NAN;
+  if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = (EXT && o.open_loop) ? jnu : NAN;
   const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
   if (lane == 0) {
     const int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
@@ -842,7 +849,9 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
-  auto kern = sc.dtc ? gpc_closed_loop_kernel<MAXM, true> : gpc_closed_loop_kernel<MAXM, false>;
+  const bool ext = o.open_loop || o.want_traj;
+  auto kern = sc.dtc ? (ext ? gpc_closed_loop_kernel<MAXM, true, true> : gpc_closed_loop_kernel<MAXM, true, false>)
+                     : (ext ? gpc_closed_loop_kernel<MAXM, false, true> : gpc_closed_loop_kernel<MAXM, false, false>);
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
