@@ -156,8 +156,9 @@ typedef struct mpct_scenario mpct_scenario;
  *   ts, nsub        Ts and the fixed RK4 sub-steps per Ts that replace ode15s / the toolbox's
  *                   discretisation (plant and prediction use the same integrator)
  *   x0[nx], u0[nu]  init.x0, init.u0
- *   u_min/u_max[nu] MV Min/Max (hard); x_min/x_max[nx] state bounds (reported through
- *                   MPCT_ST_BOUNDS, not enforced); y_scale[ny], u_scale[nu] OV / MV ScaleFactor
+ *   u_min/u_max[nu] MV Min/Max (hard); x_min/x_max[nx] hard state bounds, linearised in
+ *                   every SQP subproblem (+-inf = none; a closed loop whose states still leave
+ *                   them is flagged MPCT_ST_BOUNDS); y_scale[ny], u_scale[nu] OV / MV ScaleFactor
  *   n_max, nu_max   largest prediction / control horizon any candidate uses (nu*nu_max <= 32)
  *   nit, yref[ny*nit], vns_ink  as in mpct_scenario_desc
  *   sqp_max, sqp_tol  Gauss-Newton iteration cap per controller call and the stopping test

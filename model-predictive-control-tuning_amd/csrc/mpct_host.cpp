@@ -37,7 +37,7 @@ long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy);
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
                 LaunchFan* fan, std::string* err);
-long long nmpc_lds_bytes(int M);
+long long nmpc_lds_bytes(int M, int N);
 }  // namespace mpct
 
 using namespace mpct;
@@ -932,7 +932,7 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
 
 extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {
   if (!s) return fail(MPCT_EINVAL, "null scenario");
-  if (s->nmpc) return nmpc_lds_bytes(s->nu * Nu);
+  if (s->nmpc) return nmpc_lds_bytes(s->nu * Nu, N2);
   DevScenario ds{};
   ds.my = s->my;
   ds.nu = s->nu;

@@ -122,9 +122,10 @@ constexpr double kLsFlat = 1e-14;
 
 // LDS layout (doubles) of one simulation at QP size M
 struct NmLayout {
-  int ri, jt, ra, rr, dv, xc, u, uo, rw, cv, total;
+  int ri, jt, ra, rr, dv, xc, u, uo, rw, cv, nv, bits, xp, sx, total;
 };
-__host__ __device__ inline NmLayout nm_layout(int M) {
+// N: prediction horizon (the state-bound rows: predicted states x_i and dx_i/dv, i = 1..N)
+__host__ __device__ inline NmLayout nm_layout(int M, int N) {
   NmLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
@@ -138,9 +139,29 @@ __host__ __device__ inline NmLayout nm_layout(int M) {
   L.uo = take(M + 1);  // absolute moves of the open-loop solution (Info.MVopt)
   L.rw = take(M + 1);  // rate residuals w_u v of the current iterate
   L.cv = take(M + 1);  // c = Q'r, the rotated residual
+  L.nv = take(M + 1);  // staged normal of a state-bound row
+  L.bits = take((6 * N + 63) / 64);  // active state-bound rows (32-bit words)
+  L.xp = take(3 * N);  // predicted states x_i (i = 1..N) of the current iterate
+  L.sx = take(3 * N * M);  // their sensitivities dx_i/dv, row i*3 + s
   L.total = (o + 1) & ~1;
   return L;
 }
+
+// active flags: box rows (p < base) in the lanes' act bits, state-bound rows in an LDS bitmap
+struct StateMark {
+  unsigned* bits;
+  int base;
+  template <class St>
+  __device__ __forceinline__ void operator()(St& S, int p, bool on) const {
+    if (p < base) {
+      BoxMark{}(S, p, on);
+    } else if (threadIdx.x == 0) {
+      const int q = p - base;
+      if (on) bits[q >> 5] |= 1u << (q & 31);
+      else bits[q >> 5] &= ~(1u << (q & 31));
+    }
+  }
+};
 
 template <int MAXM>
 __global__ void __launch_bounds__(64, 1)
@@ -181,7 +202,7 @@ __global__ void __launch_bounds__(64, 1)
     return;
   }
   if (M <= mz_lo || M > MAXM) return;  // another launch's QP size class
-  const NmLayout L = nm_layout(M);
+  const NmLayout L = nm_layout(M, N);
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
@@ -192,6 +213,10 @@ __global__ void __launch_bounds__(64, 1)
   double* srw = lds + L.rw;
   double* sR = lds + L.rr;
   double* scv = lds + L.cv;
+  double* snv = lds + L.nv;
+  unsigned* sbits = reinterpret_cast<unsigned*>(lds + L.bits);
+  double* sxp = lds + L.xp;
+  double* ssx = lds + L.sx;
 
   const double* tab = sc.nm;  // [params][x0 3][u0 nu][lb nu][ub nu][xmin 3][xmax 3][sy ny][su nu]
   const VdV P = vdv_load(tab);
@@ -220,6 +245,28 @@ __global__ void __launch_bounds__(64, 1)
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 200 * M + 1000;
   const double* rr = rv + (long long)kref * ny * nit;
   long long sqp_total = 0;
+
+  // hard state bounds (VanDeVusse_NMPC.m:143-146), linearised along the prediction
+  bool has_xb = false;
+  for (int i = 0; i < 3; ++i) has_xb = has_xb || isfinite(txmin[i]) || isfinite(txmax[i]);
+  const int nbits = (6 * N + 31) / 32;
+  // d = J'n_p: box rows from gi_core's structure, state-bound rows from their staged normal
+  auto dvec = [&](int p) __attribute__((always_inline)) -> double {
+    if (p < 4 * M) {
+      const CInfo ci = cinfo(p, Nu);
+      return gi_dvec<MAXM>(sJT, sd, M, ci.j0, ci.j1, ci.sg, row);
+    }
+    const int q = p - 4 * M, r = q >> 1;
+    if (row) snv[lane] = (q & 1) ? -ssx[r * M + lane] : ssx[r * M + lane];
+    lds_sync();
+    double dk = 0.0;
+    if (row) {
+      const double* jc = sJT + lane * M;
+      for (int i = 0; i < M; ++i) dk += jc[i] * snv[i];
+      sd[lane] = dk;
+    }
+    return dk;
+  };
 
   // ---- one controller call (nlmpcmove restated): Gauss-Newton SQP from the warm start v
   // (this lane's increment), state x, last move ul[n], reference (r0, r1).  Returns v.
@@ -257,6 +304,17 @@ __global__ void __launch_bounds__(64, 1)
         double ud[2] = {0.0, 0.0};
         if (row && bl <= li) ud[bn] = 1.0;
         vdv_rk4<true>(P, h, nsub, xs, u, td, ud);
+        if (has_xb) {
+          if (row) {
+            ssx[(i * 3 + 0) * M + lane] = td[0];
+            ssx[(i * 3 + 1) * M + lane] = td[1];
+            ssx[(i * 3 + 2) * M + lane] = td[2];
+          } else if (lane == M) {
+            sxp[i * 3 + 0] = xs[0];
+            sxp[i * 3 + 1] = xs[1];
+            sxp[i * 3 + 2] = xs[2];
+          }
+        }
         for (int j = 0; j < ny; ++j) {
           const int xj = j == 0 ? xc0 : xc1;
           const double wy = j == 0 ? wy0 : wy1;
@@ -310,7 +368,9 @@ __global__ void __launch_bounds__(64, 1)
       lds_sync();
       GIState<MAXM> gis;
       gi_reset<MAXM>(gis);
+      for (int w = lane; w < nbits; w += kWave) sbits[w] = 0u;
       gi_load_rinv<MAXM>(gis, sJT, sRi, M, row);
+      const StateMark mark{sbits, 4 * M};
       int git = 0;
       for (;;) {
         const double pre = block_prefix<MAXM>(xm, bl, Nu, row, sxc);
@@ -332,6 +392,25 @@ __global__ void __launch_bounds__(64, 1)
             best = s4[k];
             bid = 4 * lane + k;
           }
+        if (has_xb) {
+          // linearised state rows  x_min <= x_i + dx_i/dv s <= x_max  at the iterate s
+          if (row) sxc[lane] = xm;
+          lds_sync();
+          for (int q = lane; q < 6 * N; q += kWave) {
+            if ((sbits[q >> 5] >> (q & 31)) & 1u) continue;
+            const int r = q >> 1, si = r - (r / 3) * 3;
+            const double bnd = (q & 1) ? txmax[si] : txmin[si];
+            if (!isfinite(bnd)) continue;
+            double dot = 0.0;
+            for (int m = 0; m < M; ++m) dot += ssx[r * M + m] * sxc[m];
+            const double xr = sxp[r] + dot;
+            const double sl = (q & 1) ? bnd - xr : xr - bnd;
+            if (sl < best) {
+              best = sl;
+              bid = 4 * M + q;
+            }
+          }
+        }
         wave_argmin64(best, bid);
         if (!(best < -tol)) break;
         if (git >= maxit) {
@@ -343,8 +422,7 @@ __global__ void __launch_bounds__(64, 1)
         bool infeas = false;
         for (;;) {
           ++git;
-          const CInfo ci = cinfo(p, Nu);
-          const double dk = gi_dvec<MAXM>(sJT, sd, M, ci.j0, ci.j1, ci.sg, row);
+          const double dk = dvec(p);
           lds_sync();
           const double d2 = row ? dk * dk : 0.0;
           const double dn2 = qsum<MAXM>(d2);
@@ -371,10 +449,10 @@ __global__ void __launch_bounds__(64, 1)
           upm += t;
           sp += t * beta;
           if (full) {
-            gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
+            gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, mark);
             break;
           }
-          gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, BoxMark{});
+          gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, mark);
           if (git >= maxit) break;
         }
         if (infeas) break;
@@ -547,7 +625,7 @@ __global__ void __launch_bounds__(64, 1)
 
 namespace mpct {
 
-long long nmpc_lds_bytes(int M) { return (long long)nm_layout(M).total * 8; }
+long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
 
 // one launch per QP size class (MAXM 16 / 32), the larger first, fanned over two streams so the
 // classes overlap (a simulation runs in the launch of its class; launch_fan.h)
@@ -562,13 +640,13 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
   FanScope fs(fan, stream);
   int nl = 0;
   if (Mmax > 16) {
-    const long long lds = nmpc_lds_bytes(Mmax);
+    const long long lds = nmpc_lds_bytes(Mmax, sc.n2max);
     hipLaunchKernelGGL(nmpc_closed_loop_kernel<32>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
                        fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 16);
   }
   {
     // mz_lo == 0 marks the status-writing launch (padding / bad horizons)
-    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax);
+    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax, sc.n2max);
     hipLaunchKernelGGL(nmpc_closed_loop_kernel<16>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
                        fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 0);
   }

@@ -33,9 +33,11 @@ replacements, so this is the oracle it is checked against (parity with MATLAB's 
   1e-14 relative count as no increase; pure Gauss-Newton
   2-cycles on this reactor's large-residual steps).  Iterate until the full step satisfies
   max_j |step_j|/s^u_j <= ``SQP_TOL`` (then taken in full) or ``SQP_MAX`` iterations.
-* OV / state bounds (soft / hard in the toolbox) are not enforced in the prediction; the
-  simulation reports whether the closed loop left them (``bounds_ok``).  The tuning grid of
-  config 5 is scored on tracking costs; see DESIGN.md §12.
+* State bounds (hard in the toolbox, ``VanDeVusse_NMPC.m:143-146``) are linearised along the
+  prediction in every Gauss-Newton subproblem (x_min <= x_i + dx_i/du d <= x_max, i = 1..N).
+  The OV bounds (``:139-142``) are the same limits on states 2:3, softened (MinECR = MaxECR = 1),
+  so the hard ones dominate and no slack is needed.  ``bounds_ok`` reports whether the closed
+  loop itself stayed inside them (the linearisation can be violated between iterations).
 """
 from __future__ import annotations
 
@@ -184,13 +186,16 @@ class NMPCResult:
     bounds_ok: bool
 
 
-def predict(x, U, N, Nu, want_sens=True):
+def predict(x, U, N, Nu, want_sens=True, states=False):
     """Outputs y(k+1..k+N) (N x NY) for absolute moves U (Nu x NU, held after Nu-1) and their
-    sensitivities dY/dU (N x NY x (Nu*NU), column n*Nu + l)."""
+    sensitivities dY/dU (N x NY x (Nu*NU), column n*Nu + l); states=True also returns the
+    predicted states (N x 3) and their sensitivities (N x 3 x M)."""
     M = NU * Nu
     X = np.zeros((3, M))
     Y = np.zeros((N, NY))
     S = np.zeros((N, NY, M))
+    XP = np.zeros((N, 3))
+    SX = np.zeros((N, 3, M))
     for i in range(N):
         li = min(i, Nu - 1)
         u = U[li]
@@ -200,9 +205,13 @@ def predict(x, U, N, Nu, want_sens=True):
                 Ud[n, n * Nu + li] = 1.0
             x, X = rk4(x, u, (X, Ud))
             S[i] = X[1:]
+            SX[i] = X
         else:
             x = rk4(x, u)
         Y[i] = x[1:]
+        XP[i] = x
+    if states:
+        return Y, S, XP, SX
     return Y, S
 
 
@@ -213,9 +222,14 @@ def cost(x, U, u_last, rvec, N, Nu, wy, wu):
     return 0.5 * float(np.sum(((Y - rvec[None, :]) * wy[None, :]) ** 2) + np.sum((du * wu[None, :]) ** 2))
 
 
-def controller(x, u_last, rvec, N, Nu, delta, lam, U_init):
-    """One nlmpcmove restated (see module docstring).  Returns (U, iterations)."""
+def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None):
+    """One nlmpcmove restated (see module docstring).  xbounds = (x_min, x_max): hard state
+    bounds (VanDeVusse_NMPC.m:143-146; the OV bounds of :139-142 are the same limits on states
+    2:3, softened, so the hard ones dominate), linearised along the prediction in every
+    Gauss-Newton subproblem.  Returns (U, iterations)."""
     from scipy.optimize import lsq_linear
+
+    from .toolbox_band import qp_dual_dense
 
     wy = np.abs(delta) / SY          # toolbox weights over ScaleFactors, squared in the cost
     wu = np.abs(lam) / SU
@@ -224,7 +238,7 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init):
     su = np.repeat(SU, Nu)
     it = 0
     for it in range(1, SQP_MAX + 1):
-        Y, S = predict(x, U, N, Nu)
+        Y, S, XP, SX = predict(x, U, N, Nu, states=True)
         # residuals: outputs (i, j) then moves (n, l), variables v[n*Nu + l] = U[l, n]
         ry = ((Y - rvec[None, :]) * wy[None, :]).reshape(-1)
         Jy = (S * wy[None, :, None]).reshape(N * NY, M)
@@ -246,6 +260,24 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init):
         lo = np.minimum(lo, 0.0)   # the iterate is feasible up to rounding
         hi = np.maximum(hi, 0.0)
         d = lsq_linear(A, -res, bounds=(lo, hi), method="bvls", tol=1e-14, lsmr_tol=None).x
+        if xbounds is not None:
+            # linearised state rows  x_min <= x_i + SX_i d <= x_max  (i = 1..N); when the bounded
+            # least-squares step violates one, the whole QP is re-solved with them (unique optimum)
+            xmn, xmx = (np.asarray(b_, dtype=float) for b_ in xbounds)
+            rows, rhs = [], []
+            for i in range(N):
+                for s in range(3):
+                    if np.isfinite(xmn[s]):
+                        rows.append(SX[i, s]); rhs.append(xmn[s] - XP[i, s])
+                    if np.isfinite(xmx[s]):
+                        rows.append(-SX[i, s]); rhs.append(XP[i, s] - xmx[s])
+            if rows:
+                Ac, bc = np.array(rows), np.array(rhs)
+                if np.min(Ac @ d - bc) < -1e-10 * max(1.0, float(np.max(np.abs(bc)))):
+                    I = np.eye(M)
+                    Aall = np.vstack([I, -I, Ac])
+                    ball = np.concatenate([lo, -hi, bc])
+                    d, _, _ = qp_dual_dense(A, res, Aall, ball, qr=True)
         lo_b, hi_b = np.repeat(LB, Nu), np.repeat(UB, Nu)
         if np.max(np.abs(d) / su) <= SQP_TOL:
             v = np.clip(v + d, lo_b, hi_b)
@@ -270,7 +302,7 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init):
 
 
 def closedloop_nmpc(r, N: int, Nu: int, delta, lam, nit: int = NIT, x0=None, u0=U0,
-                    open_loop: bool = True) -> NMPCResult:
+                    open_loop: bool = True, xbounds=(XMIN, XMAX)) -> NMPCResult:
     """[y,u,yopt,uopt] = closedloop_toolbox_nmpc(nmpcobj,model,init,r,N,Nu,delta,lambda,nit)."""
     x0 = steady_state() if x0 is None else np.asarray(x0, dtype=float)
     r = np.asarray(r, dtype=float).reshape(NY, nit)
@@ -283,17 +315,18 @@ def closedloop_nmpc(r, N: int, Nu: int, delta, lam, nit: int = NIT, x0=None, u0=
     Uw = np.tile(np.asarray(u0, dtype=float), (Nu, 1))
     iters = 0
     for i in range(1, nit):
-        Uw, it = controller(X[:, i - 1], U[:, i - 1], r[:, i], N, Nu, delta, lam, Uw)
+        Uw, it = controller(X[:, i - 1], U[:, i - 1], r[:, i], N, Nu, delta, lam, Uw, xbounds)
         iters += it
         U[:, i] = Uw[0]
         X[:, i] = rk4(X[:, i - 1], U[:, i])
         Y[:, i] = X[1:, i]
         Uw = np.vstack([Uw[1:], Uw[-1:]])            # warm start: shift by one move
-    ok = bool(np.all(X >= XMIN[:, None] - 1e-9) and np.all(X <= XMAX[:, None] + 1e-9))
+    xmn, xmx = (np.asarray(b_, dtype=float) for b_ in (xbounds if xbounds is not None else (XMIN, XMAX)))
+    ok = bool(np.all(X >= xmn[:, None] - 1e-9) and np.all(X <= xmx[:, None] + 1e-9))
     yopt = uopt = None
     if open_loop:
         Uo, it = controller(x0, np.asarray(u0, dtype=float), r[:, -1], N, Nu, delta, lam,
-                            np.tile(np.asarray(u0, dtype=float), (Nu, 1)))
+                            np.tile(np.asarray(u0, dtype=float), (Nu, 1)), xbounds)
         iters += it
         # MVopt: p+1 rows (moves held after Nu), padded with its last row to nit
         uo = np.array([Uo[min(k, Nu - 1)] for k in range(nit)])

@@ -167,7 +167,7 @@ def qp_primal_active_set_x0(W, c, Ain, bin_, x0, tol=1e-12, maxit=2000):
     raise RuntimeError("primal active set did not converge")
 
 
-def qp_dual_dense(W, c, A, b, tol=1e-12, maxit=5000):
+def qp_dual_dense(W, c, A, b, tol=1e-12, maxit=5000, qr=False):
     """min 1/2 ||W x + c||^2 s.t. A x >= b by the textbook dual method of Goldfarb & Idnani
     (1983), recomputed densely at every iteration: in the coordinates w = L'x (H = W'W = LL')
     the Hessian is I, the primal direction is the projection of n_p onto null(N_A) and the dual
@@ -176,14 +176,21 @@ def qp_dual_dense(W, c, A, b, tol=1e-12, maxit=5000):
     every addition the iterate is re-solved exactly on the active set.  No factor updates and no
     warm start: the device's J-form / Householder / warm-started variant shares none of this
     arithmetic.  The dual objective increases monotonically, so the ~1.8k near-parallel output
-    rows of the N2 = 127 range cannot make it cycle.  Returns (x, iterations, active set)."""
+    rows of the N2 = 127 range cannot make it cycle.  Returns (x, iterations, active set).
+    qr=True: the factor comes from a QR of W (H = R'R, L = R') instead of a Cholesky of W'W --
+    for least-squares problems whose W'W is too ill-conditioned to form (the NMPC's, cond ~1e15)."""
     import scipy.linalg as sla
 
-    H = W.T @ W
-    g = W.T @ c
-    L = np.linalg.cholesky(H)
+    if qr:
+        Qw, Rw = np.linalg.qr(W)
+        L = Rw.T
+        gw = Qw.T @ c
+    else:
+        H = W.T @ W
+        g = W.T @ c
+        L = np.linalg.cholesky(H)
+        gw = sla.solve_triangular(L, g, lower=True)
     Aw = sla.solve_triangular(L, A.T, lower=True).T          # rows of A L^-T
-    gw = sla.solve_triangular(L, g, lower=True)
     w = -gw
     act, u = [], np.zeros(0)
     it = 0

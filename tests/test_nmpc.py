@@ -89,6 +89,28 @@ def test_nmpc_oracle_controller_is_optimal():
     assert np.max(np.abs(pg)) < 1e-8 * max(1.0, np.max(np.abs(g))), pg
 
 
+XMAX_TIGHT = np.array([6.0, 1.2, 135.0])   # T <= 135: active after the 130-degree setpoint step
+
+
+def test_nmpc_oracle_state_bounds_hold():
+    """Hard state bounds (VanDeVusse_NMPC.m:143-146 OutputVariables/States Min/Max): candidate 2
+    of the seeded grid overshoots T = 135 without them (135.2) and stays on the bound with them."""
+    import oracle.nmpc_vdv as nv
+    from mpct.nmpc import nmpc_candidate_grid
+
+    N, Nu, d, lam = nmpc_candidate_grid(64)
+    x0 = nv.steady_state()
+    r, _ = nv.references(x0)
+    k = 2
+    free = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], open_loop=False,
+                              xbounds=(nv.XMIN, np.full(3, np.inf)))
+    held = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], open_loop=False,
+                              xbounds=(nv.XMIN, XMAX_TIGHT))
+    assert free.y[1].max() > 135.1
+    assert held.bounds_ok and held.y[1].max() <= 135.0 + 1e-8
+    assert held.y[1].max() > 135.0 - 1e-6   # the bound is active, not merely respected
+
+
 def test_nmpc_product_setup_matches_oracle(built):
     import oracle.nmpc_vdv as nv
     from mpct import nmpc
@@ -154,6 +176,32 @@ def test_nmpc_gpu_matches_oracle(gpu):
             xr = np.abs(o.uopt[:, :1]) / du
         xr[~np.isfinite(xr)] = 0.0
         np.testing.assert_allclose(res.Jnu[k], (xr ** 2).sum(1), rtol=COST_RTOL)
+
+
+@pytest.mark.gpu
+def test_nmpc_gpu_state_bounds_match_oracle(gpu):
+    """Tight T bound: the linearised state rows enter the kernel's QP as general constraints
+    (LDS bitmap of active rows, staged normals); the loops equal the oracle's re-solve."""
+    import oracle.nmpc_vdv as nv
+    from mpct.engine import eval_batch
+    from mpct import nmpc
+
+    x0 = nmpc.steady_state()
+    r, yref = nmpc.vandevusse_signals(x0)
+    # ScaleFactors stay the nominal OV ranges (VanDeVusse_NMPC.m:151,159): only the bound moves
+    sc = nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, XMAX_TIGHT,
+                           yref, 31, 15, y_scale=nv.SY)
+    N, Nu, d, lam = nmpc.nmpc_candidate_grid(64)
+    pick = [2, 6, 0]
+    res = eval_batch(sc, N[pick], Nu[pick], d[pick], lam[pick], r[None], open_loop=True, want_traj=True)
+    assert np.all(res.status == 0), res.status
+    for s, k in enumerate(pick):
+        o = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], xbounds=(nv.XMIN, XMAX_TIGHT))
+        assert o.bounds_ok
+        for a, b in ((res.y[s], o.y), (res.u[s], o.u), (res.ys[s], o.yopt), (res.uopt[s], o.uopt)):
+            assert _trel(a, b) < TRAJ_RTOL, (k, _trel(a, b))
+        np.testing.assert_allclose(res.J1[s], ((o.y - yref) ** 2).sum(1), rtol=COST_RTOL)
+        assert res.y[s][1].max() <= 135.0 + 1e-8
 
 
 @pytest.mark.gpu
