@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(64, 1)
     nmpc_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ Nv,
                             const int* __restrict__ Nuv, const double* __restrict__ deltav,
                             const double* __restrict__ lambdav, const double* __restrict__ rv, const DevOpts o,
-                            const DevResult out, int mz_lo) {
+                            const DevResult out, int mz_lo, long long lds_lo, long long lds_hi, int first_) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const long long sim = blockIdx.x;
@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(64, 1)
       if (out.qp_iters) out.qp_iters[sim] = 0;
     }
   };
-  const bool first = mz_lo == 0;
+  const bool first = first_ != 0;
   if (N <= 0) {
     if (first) write_nan(MPCT_ST_SKIPPED_);
     return;
@@ -203,6 +203,7 @@ __global__ void __launch_bounds__(64, 1)
   }
   if (M <= mz_lo || M > MAXM) return;  // another launch's QP size class
   const NmLayout L = nm_layout(M, N);
+  if ((long long)L.total * 8 <= lds_lo || (long long)L.total * 8 > lds_hi) return;  // another LDS tier
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
@@ -621,14 +622,40 @@ __global__ void __launch_bounds__(64, 1)
 
 // ------------------------------------------------------------------------------------------
 // host-side launch
+#include <algorithm>
 #include <string>
 
 namespace mpct {
 
 long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
 
-// one launch per QP size class (MAXM 16 / 32), the larger first, fanned over two streams so the
-// classes overlap (a simulation runs in the launch of its class; launch_fan.h)
+// one launch per (QP size class MAXM 16 / 32) x (LDS tier), heaviest first, fanned over the
+// streams of launch_fan.h so the tiers overlap; a simulation runs in the launch of its class and
+// tier, and the light tiers (short horizons) get the occupancy their own LDS allows instead of
+// the n_max-sized allocation of the heaviest candidate
+template <int MAXM>
+static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
+                         const double* lambda, const double* r, const DevOpts& o, const DevResult& out, FanScope& fs,
+                         int& nl, int mz_lo, bool& first, std::string* err) {
+  const int Mhi = std::min(sc.nu * sc.numax, MAXM);
+  const long long lds_max = nmpc_lds_bytes(Mhi, sc.n2max);
+  // 12 / 6 waves per CU for the small class, 5 / 2 for the large one
+  const long long cap = MAXM <= 16 ? 13 * 1024 : 32 * 1024;
+  const long long lo[2] = {0, cap}, hi[2] = {std::min(cap, lds_max), lds_max};
+  for (int k = (lds_max > cap ? 1 : 0); k >= 0; --k) {
+    hipLaunchKernelGGL(nmpc_closed_loop_kernel<MAXM>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)hi[k],
+                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, mz_lo, lo[k], hi[k],
+                       first ? 1 : 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
+      return -3;
+    }
+    first = false;
+  }
+  return 0;
+}
+
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
                 LaunchFan* fan, std::string* err) {
@@ -637,26 +664,17 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
     *err = "nu*nu_max > 32";
     return -4;
   }
+  if (nmpc_lds_bytes(Mmax, sc.n2max) > 64 * 1024) {
+    *err = "n_max x nu*nu_max needs more than 64 KiB of LDS per simulation";
+    return -4;
+  }
   FanScope fs(fan, stream);
-  int nl = 0;
-  if (Mmax > 16) {
-    const long long lds = nmpc_lds_bytes(Mmax, sc.n2max);
-    hipLaunchKernelGGL(nmpc_closed_loop_kernel<32>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
-                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 16);
-  }
-  {
-    // mz_lo == 0 marks the status-writing launch (padding / bad horizons)
-    const long long lds = nmpc_lds_bytes(16 < Mmax ? 16 : Mmax, sc.n2max);
-    hipLaunchKernelGGL(nmpc_closed_loop_kernel<16>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds,
-                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, 0);
-  }
+  int nl = 0, rc = 0;
+  bool first = true;  // the first launch also writes the padding / bad-horizon statuses
+  if (Mmax > 16) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, o, out, fs, nl, 16, first, err);
+  if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, o, out, fs, nl, 0, first, err);
   fs.join();
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
-    return -3;
-  }
-  return 0;
+  return rc;
 }
 
 }  // namespace mpct
