@@ -45,6 +45,18 @@ def algorithmic_flops_per_sim(sc, N2, Nu, iters_per_step):
     return setup + sc.nit * per_step
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (report the baseline's cores and CPU model)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,8 +201,9 @@ def main():
         cpu = {"value": passes * ncpu / tc, "unit": "sims/s", "cores": threads, "kind": "port",
                "sample": "oracle/cgpc.c on the same %d-candidate Shell 3x3 batch (N2=%d, Nu=%d, nit=500), "
                          "%d passes, %d OpenMP threads, %.2f s wall (%.0f thread-s); max rel "
-                         "|J1_gpu - J1_cpu| = %.1e" % (ncpu, args.n2, args.nu, passes, threads, tc,
-                                                       tc * threads, rel)}
+                         "|J1_gpu - J1_cpu| = %.1e; host %s, %d logical CPUs visible"
+                         % (ncpu, args.n2, args.nu, passes, threads, tc, tc * threads, rel, cpu_model(),
+                            os.cpu_count() or 0)}
 
     line = {
         "metric": "closed-loop GPC sims/sec (Shell 3x3, N2=30 Nu=5) over tuning grid",
