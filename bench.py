@@ -45,6 +45,63 @@ def algorithmic_flops_per_sim(sc, N2, Nu, iters_per_step):
     return setup + sc.nit * per_step
 
 
+def other_cpu_baseline(workload, N2, Nu, d, l, refs, J1, st, seconds):
+    """Single-thread CPU restatement (oracle/) of a config-3/4/5 simulation, timed on a bounded
+    seeded sample of the same grid (rank 0, N = 1): the reference-structured numpy loops, i.e.
+    toolbox_band.closedloop_band (config 3), nmpc_vdv.closedloop_nmpc (config 5) and
+    dtcgpc.dtc_gpc_ww (config 4: DTC_GPC_WW.m's full-history lsim loop, nominal plant)."""
+    rel = []
+    if workload == "shell7x5":
+        from oracle.scenarios import shell7x5 as o_shell7x5
+        from oracle.toolbox_band import closedloop_band
+
+        osc, orr, ov, _, _ = o_shell7x5()
+        what = "oracle/toolbox_band.py closedloop_band (numpy, nit=200, closed loop only)"
+
+        def run(k):
+            closedloop_band(osc, orr, ov, int(N2[k]), int(Nu[k]), d[k], l[k], orr.shape[1], open_loop=False)
+    elif workload == "vandevusse":
+        from mpct.nmpc import steady_state, vandevusse_signals
+        from oracle.nmpc_vdv import closedloop_nmpc
+
+        _, yref = vandevusse_signals(steady_state())
+        what = "oracle/nmpc_vdv.py closedloop_nmpc (numpy, nit=60 + open loop)"
+
+        def run(k):
+            o = closedloop_nmpc(refs[0], int(N2[k]), int(Nu[k]), d[k], l[k])
+            if st[k] == 0:
+                j1 = ((o.y - yref) ** 2).sum(1)
+                rel.append(float(np.max(np.abs(J1[k] - j1) / np.maximum(np.abs(j1), 1e-300))))
+    else:
+        from oracle.dtcgpc import dtc_gpc_ww
+
+        what = "oracle/dtcgpc.py dtc_gpc_ww (numpy, DTC_GPC_WW.m full-history lsim loop, nominal plant)"
+
+        def run(k):
+            p, m = int(N2[k]), int(Nu[k])
+            dtc_gpc_ww(p=(p, p), m=(m, m), lam=tuple(l[k]), delta=tuple(d[k]))
+    done, tc, picked = 0, 0.0, []
+    for k in np.random.default_rng(20250307).permutation(len(N2)):
+        k = int(k)
+        t1 = time.perf_counter()
+        try:
+            run(k)
+        except RuntimeError:
+            continue  # an oracle self-check that gives up (toolbox_band's KKT NNLS) is not timed
+        tc += time.perf_counter() - t1
+        done += 1
+        picked.append("%d/%d" % (N2[k], Nu[k]))
+        if tc >= seconds:
+            break
+    if not done:
+        return None
+    sample = "%s on %d seeded random grid candidates (N/Nu %s), 1 thread, %.1f s" % (
+        what, done, " ".join(picked), tc)
+    if rel:
+        sample += "; max rel |J1_gpu - J1_cpu| = %.1e" % max(rel)
+    return {"value": done / tc, "unit": "sims/s", "cores": 1, "kind": "port", "sample": sample}
+
+
 def cpu_model() -> str:
     """The host CPU's model name (report the baseline's cores and CPU model)."""
     try:
@@ -345,13 +402,17 @@ def other_workload(args):
         elapsed = float(te.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     st = out["status"].cpu().numpy()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = other_cpu_baseline(args.workload, N2, Nu, d, l, refs, out["J1"].cpu().numpy(), st,
+                                 args.cpu_seconds)
     if rank == 0:
         sims = (Cg * nref if scaling == "strong" else world * S) * steps
         line = {"metric": metric, "value": sims / elapsed, "unit": "sims/s", "n_gpus": world, "steps": steps,
                 "warmup": warm, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f64", "data": "synthetic candidate grid (seed 20250307) on the "
                 "reference's scenario", "config": dict(cfg, parallelism="dp%d" % world),
-                "roofline": None, "kernel_ms_rank0": kms, "cpu_baseline": None,
+                "roofline": None, "kernel_ms_rank0": kms, "cpu_baseline": cpu,
                 "status_codes": {int(k): int(n) for k, n in zip(*np.unique(st, return_counts=True))},
                 "top_candidate": int(order[0].item())}
         print(json.dumps(line), flush=True)
