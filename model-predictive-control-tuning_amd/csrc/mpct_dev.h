@@ -5,6 +5,14 @@
 
 namespace mpct {
 
+// device buffers of the dispatch-order sort (keys, indices, hipcub temp), owned by a scenario
+struct WorkOrder {
+  void* buf = nullptr;
+  size_t bytes = 0;
+};
+constexpr long long kOrderMinC = 256;  // at most one workgroup per CU: a single round, order is moot
+
+
 constexpr int kMaxOut = 16;    // outputs (my)
 constexpr int kMaxIn = 16;     // inputs (nu + nd)
 constexpr int kURing = 32;     // plant input history ring (power of two)

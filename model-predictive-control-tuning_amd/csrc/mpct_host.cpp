@@ -26,7 +26,7 @@ namespace mpct {
 int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                        const double* delta, const double* lambda, const double* r,
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
-                       hipStream_t stream, std::string* err);
+                       WorkOrder* wo, hipStream_t stream, std::string* err);
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
 // defined in mdband_kernel.hip
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
@@ -90,6 +90,7 @@ struct mpct_scenario {
   // scratch buffers for the host-pointer API (grow only)
   void* dscratch = nullptr;
   LaunchFan fan;  // auxiliary streams of the class launches (band / NMPC kernels)
+  WorkOrder order;  // dispatch-order sort buffers (GPC kernel)
   size_t dscratch_bytes = 0;
 };
 
@@ -606,6 +607,7 @@ extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
     if (hipGetDevice(&cur) == hipSuccess && s->dev >= 0) (void)hipSetDevice(s->dev);
     if (s->dtab) (void)hipFree(s->dtab);
     if (s->dscratch) (void)hipFree(s->dscratch);
+    if (s->order.buf) (void)hipFree(s->order.buf);
     s->fan.release();
     if (cur >= 0) (void)hipSetDevice(cur);
   }
@@ -671,6 +673,10 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
     (void)hipFree(s->dscratch);
     s->dscratch = nullptr;
     s->dscratch_bytes = 0;
+  }
+  if (s->order.buf) {
+    (void)hipFree(s->order.buf);
+    s->order = WorkOrder{};
   }
   // pack all tables into one allocation, 256-B aligned pieces
   std::vector<char> blob;
@@ -826,7 +832,7 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
     rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream),
                        &s->fan, &err);
   else
-    rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax,
+    rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &s->order,
                             static_cast<hipStream_t>(stream), &err);
   if (rc) return fail(rc, err);
 #ifdef MPCT_PROFILE

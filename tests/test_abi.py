@@ -195,6 +195,8 @@ def _kernel_meta(text):
     for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, flags=re.S):
         body = m.group(2)
         mm = re.search(r"kernelILi(\d+)ELb(\d)E", m.group(1))
+        if mm is None:  # helper kernels of the file (dispatch-order keys, hipcub's radix sort)
+            continue
         out[(int(mm.group(1)), int(mm.group(2)))] = dict(
             scratch=int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", body).group(1)),
             vgpr=int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", body).group(1)))

@@ -130,7 +130,8 @@ def test_gpc_window_unsquared_and_rounded(env, built):
 
 def test_full_grid_properties(env):
     """Full metric batch (4096 candidates): clean status, finite costs, bitwise determinism and
-    independence from batch order / composition."""
+    independence from batch order / composition (the library dispatches the candidates in its own
+    heaviest-first order, gpc_kernel.hip order_candidates; results stay in the caller's order)."""
     from mpct.engine import eval_batch
     from mpct.scenarios import candidate_grid
 
