@@ -831,7 +831,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
 // host-side launch
 #include <string>
 
-#include <hipcub/hipcub.hpp>
+#include "work_order.h"
 
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
@@ -844,74 +844,6 @@ long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {
   const int M = sc.nu * Nu;
   LdsLayout L = lds_layout(sc, M);
   return (long long)L.total * 8;
-}
-
-// ---- dispatch order (longest-processing-time first).  The workgroups of a launch start in slot
-// order and a batch larger than the resident slots (4096 simulations, 12 slots per CU at the
-// metric) runs a second, partial round, so a long simulation that starts late sets the kernel
-// time.  Simulation time grows with the QP size M and with the QP work, which the candidates'
-// weights predict: the more the tracking weights dominate the move-rate weights, the more often
-// the bounds bind.  Key (ascending = heavier first): ~(M << 20 | q(mean_j log2(max_i|delta_i| /
-// |lambda_j|))); invalid candidates last.  Measured on the metric batch (tools/order_probe.py):
-// grid order 5.36 ms, this key 3.9 ms, ideal (measured QP work, descending) 3.58 ms.
-__global__ void order_keys(long long C, int my, int nu, const int* __restrict__ N2, const int* __restrict__ Nu,
-                           const double* __restrict__ delta, const double* __restrict__ lambda,
-                           unsigned* __restrict__ key, int* __restrict__ idx) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  unsigned k = 0xffffffffu;
-  const int n2 = N2[c], nuc = Nu[c];
-  if (n2 > 0 && nuc > 0 && nuc <= 64) {
-    double dmax = 0.0;
-    for (int i = 0; i < my; ++i) dmax = fmax(dmax, fabs(delta[c * my + i]));
-    double a = 0.0;
-    for (int j = 0; j < nu; ++j) a += log2(fmax(dmax, 1e-300) / fmax(fabs(lambda[c * nu + j]), 1e-300));
-    a /= nu;
-    const double qd = fmin(fmax((a + 256.0) * 2048.0, 0.0), 1048575.0);
-    const unsigned M = (unsigned)(nu * nuc);
-    k = ~((M << 20) | (unsigned)qd);
-  }
-  key[c] = k;
-  idx[c] = (int)c;
-}
-
-static int order_candidates(const DevScenario& sc, long long C, const int* N2, const int* Nu, const double* delta,
-                            const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream,
-                            std::string* err) {
-  *perm = nullptr;
-  if (C < kOrderMinC) return 0;  // one round of workgroups: the order cannot matter
-  size_t temp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                         (const int*)nullptr, (int*)nullptr, (int)C) != hipSuccess) {
-    *err = "hipcub::DeviceRadixSort::SortPairs (size query) failed";
-    return -3;
-  }
-  const size_t arr = ((size_t)C * 4 + 255) & ~(size_t)255;
-  const size_t need = 4 * arr + temp;
-  if (need > wo.bytes) {
-    if (wo.buf) (void)hipFree(wo.buf);
-    wo.buf = nullptr;
-    wo.bytes = 0;
-    if (hipMalloc(&wo.buf, need) != hipSuccess) {
-      *err = "hipMalloc failed (dispatch-order buffers)";
-      return -2;
-    }
-    wo.bytes = need;
-  }
-  char* b = static_cast<char*>(wo.buf);
-  unsigned* kin = reinterpret_cast<unsigned*>(b);
-  unsigned* kout = reinterpret_cast<unsigned*>(b + arr);
-  int* iin = reinterpret_cast<int*>(b + 2 * arr);
-  int* iout = reinterpret_cast<int*>(b + 3 * arr);
-  hipLaunchKernelGGL(order_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, C, sc.my, sc.nu, N2, Nu,
-                     delta, lambda, kin, iin);
-  if (hipcub::DeviceRadixSort::SortPairs(b + 4 * arr, temp, kin, kout, iin, iout, (int)C, 0, 32, stream) !=
-      hipSuccess) {
-    *err = "hipcub::DeviceRadixSort::SortPairs failed";
-    return -3;
-  }
-  *perm = iout;
-  return 0;
 }
 
 template <int MAXM>
@@ -955,7 +887,7 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
   }
   const int* perm = nullptr;
   if (wo) {
-    const int rc = order_candidates(sc, C, N2, Nu, delta, lambda, *wo, &perm, stream, err);
+    const int rc = order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err);
     if (rc) return rc;
   }
   if (maxM <= 16) return launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);

@@ -36,7 +36,7 @@ long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy);
 // defined in nmpc_kernel.hip
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
-                LaunchFan* fan, std::string* err);
+                LaunchFan* fan, WorkOrder* wo, std::string* err);
 long long nmpc_lds_bytes(int M, int N);
 }  // namespace mpct
 
@@ -90,7 +90,7 @@ struct mpct_scenario {
   // scratch buffers for the host-pointer API (grow only)
   void* dscratch = nullptr;
   LaunchFan fan;  // auxiliary streams of the class launches (band / NMPC kernels)
-  WorkOrder order;  // dispatch-order sort buffers (GPC kernel)
+  WorkOrder order;  // dispatch-order sort buffers (GPC and NMPC kernels)
   size_t dscratch_bytes = 0;
 };
 
@@ -827,7 +827,7 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   std::string err;
   if (s->nmpc)
     rc = launch_nmpc(s->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, static_cast<hipStream_t>(stream), &s->fan,
-                     &err);
+                     &s->order, &err);
   else if (s->mdband)
     rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream),
                        &s->fan, &err);

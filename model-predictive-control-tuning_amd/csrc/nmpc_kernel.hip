@@ -167,14 +167,18 @@ template <int MAXM>
 __global__ void __launch_bounds__(64, 1)
     nmpc_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ Nv,
                             const int* __restrict__ Nuv, const double* __restrict__ deltav,
-                            const double* __restrict__ lambdav, const double* __restrict__ rv, const DevOpts o,
+                            const double* __restrict__ lambdav, const double* __restrict__ rv,
+                            const int* __restrict__ perm, const DevOpts o,
                             const DevResult out, int mz_lo, long long lds_lo, long long lds_hi, int first_) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
-  const long long sim = blockIdx.x;
-  if (sim >= C * nref) return;
-  const long long c = sim / nref;
-  const int kref = (int)(sim - c * nref);
+  // workgroup slot -> candidate (heaviest estimated work first, work_order.h) or identity
+  const long long slot = blockIdx.x;
+  if (slot >= C * nref) return;
+  const long long cs = slot / nref;
+  const int kref = (int)(slot - cs * nref);
+  const long long c = perm ? (long long)perm[cs] : cs;
+  const long long sim = c * nref + kref;
   const int ny = sc.my, nu = sc.nu, nit = sc.nit;
   const int N = Nv[c], Nu = Nuv[c];
   const int M = nu * Nu;
@@ -625,6 +629,8 @@ __global__ void __launch_bounds__(64, 1)
 #include <algorithm>
 #include <string>
 
+#include "work_order.h"
+
 namespace mpct {
 
 long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
@@ -635,8 +641,8 @@ long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total
 // the n_max-sized allocation of the heaviest candidate
 template <int MAXM>
 static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
-                         const double* lambda, const double* r, const DevOpts& o, const DevResult& out, FanScope& fs,
-                         int& nl, int mz_lo, bool& first, std::string* err) {
+                         const double* lambda, const double* r, const int* perm, const DevOpts& o,
+                         const DevResult& out, FanScope& fs, int& nl, int mz_lo, bool& first, std::string* err) {
   const int Mhi = std::min(sc.nu * sc.numax, MAXM);
   const long long lds_max = nmpc_lds_bytes(Mhi, sc.n2max);
   // 12 / 6 waves per CU for the small class, 5 / 2 for the large one
@@ -644,7 +650,7 @@ static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int
   const long long lo[2] = {0, cap}, hi[2] = {std::min(cap, lds_max), lds_max};
   for (int k = (lds_max > cap ? 1 : 0); k >= 0; --k) {
     hipLaunchKernelGGL(nmpc_closed_loop_kernel<MAXM>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)hi[k],
-                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, o, out, mz_lo, lo[k], hi[k],
+                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, mz_lo, lo[k], hi[k],
                        first ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -658,7 +664,7 @@ static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int
 
 int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, hipStream_t stream,
-                LaunchFan* fan, std::string* err) {
+                LaunchFan* fan, WorkOrder* wo, std::string* err) {
   const int Mmax = sc.nu * sc.numax;
   if (Mmax > 32) {
     *err = "nu*nu_max > 32";
@@ -668,11 +674,16 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
     *err = "n_max x nu*nu_max needs more than 64 KiB of LDS per simulation";
     return -4;
   }
-  FanScope fs(fan, stream);
+  const int* perm = nullptr;
+  if (wo) {
+    const int rc0 = order_candidates(kOrderNmpc, sc.my, sc.nu, C, N, Nu, delta, lambda, *wo, &perm, stream, err);
+    if (rc0) return rc0;
+  }
+  FanScope fs(fan, stream);  // forks after the sort: every class launch waits for the permutation
   int nl = 0, rc = 0;
   bool first = true;  // the first launch also writes the padding / bad-horizon statuses
-  if (Mmax > 16) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, o, out, fs, nl, 16, first, err);
-  if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, o, out, fs, nl, 0, first, err);
+  if (Mmax > 16) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 16, first, err);
+  if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);
   fs.join();
   return rc;
 }

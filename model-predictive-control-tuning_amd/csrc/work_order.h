@@ -1,0 +1,26 @@
+// work_order.h — heaviest-first dispatch order of a batch of candidates (host side).
+//
+// The closed-loop kernels run one simulation per workgroup and their batches overfill the
+// resident slots, so the last round of workgroups starts as slots free up; a long simulation that
+// starts late sets the kernel time.  order_candidates sorts the candidates by an a-priori work
+// key (longest-processing-time first) and hands the kernels a permutation slot -> candidate; the
+// results stay in the caller's order.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "mpct_dev.h"
+
+namespace mpct {
+
+enum OrderKind {
+  kOrderGpc = 0,   // GPC / DTC-GPC: QP size M, then the tracking-to-move weight ratio (more QP work)
+  kOrderNmpc = 1,  // NMPC: horizon N and the weight ratio (fewer Gauss-Newton iterations)
+};
+
+// perm = nullptr when the batch is too small for the order to matter (kOrderMinC)
+int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
+                     const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err);
+
+}  // namespace mpct
