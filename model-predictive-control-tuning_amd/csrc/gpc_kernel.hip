@@ -890,9 +890,12 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const int rc = order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err);
     if (rc) return rc;
   }
-  if (maxM <= 16) return launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
-  if (maxM <= 32) return launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
-  return launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
+  int rc;
+  if (maxM <= 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
+  else if (maxM <= 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
+  else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
+  if (perm) order_mark_used(*wo, stream);
+  return rc;
 }
 
 }  // namespace mpct

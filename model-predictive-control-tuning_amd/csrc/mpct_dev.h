@@ -6,9 +6,13 @@
 namespace mpct {
 
 // device buffers of the dispatch-order sort (keys, indices, hipcub temp), owned by a scenario
+// The permutation is read by the launch that follows the sort; `used` is recorded after that
+// launch so that the next call's sort (possibly on another stream) waits before rewriting it.
 struct WorkOrder {
   void* buf = nullptr;
   size_t bytes = 0;
+  hipEvent_t used = nullptr;
+  bool pending = false;  // `used` has been recorded
 };
 constexpr long long kOrderMinC = 256;  // at most one workgroup per CU: a single round, order is moot
 

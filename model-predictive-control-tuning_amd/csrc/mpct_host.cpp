@@ -19,6 +19,7 @@
 
 #include "../../include/mpct.h"
 #include "launch_fan.h"
+#include "work_order.h"
 #include "mpct_dev.h"
 
 namespace mpct {
@@ -607,7 +608,7 @@ extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
     if (hipGetDevice(&cur) == hipSuccess && s->dev >= 0) (void)hipSetDevice(s->dev);
     if (s->dtab) (void)hipFree(s->dtab);
     if (s->dscratch) (void)hipFree(s->dscratch);
-    if (s->order.buf) (void)hipFree(s->order.buf);
+    order_release(s->order);
     s->fan.release();
     if (cur >= 0) (void)hipSetDevice(cur);
   }
@@ -674,10 +675,7 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
     s->dscratch = nullptr;
     s->dscratch_bytes = 0;
   }
-  if (s->order.buf) {
-    (void)hipFree(s->order.buf);
-    s->order = WorkOrder{};
-  }
+  order_release(s->order);
   // pack all tables into one allocation, 256-B aligned pieces
   std::vector<char> blob;
   auto put = [&](const void* p, size_t bytes) -> size_t {

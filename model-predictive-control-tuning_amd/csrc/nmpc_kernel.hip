@@ -685,6 +685,7 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
   if (Mmax > 16) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 16, first, err);
   if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);
   fs.join();
+  if (perm) order_mark_used(*wo, stream);  // after the join: every class launch has read it
   return rc;
 }
 

@@ -23,4 +23,8 @@ enum OrderKind {
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err);
 
+// after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
+void order_mark_used(WorkOrder& wo, hipStream_t stream);
+void order_release(WorkOrder& wo);
+
 }  // namespace mpct

@@ -51,6 +51,10 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err) {
   *perm = nullptr;
   if (C < kOrderMinC) return 0;  // one round of workgroups: the order cannot matter
+  if (wo.pending && hipStreamWaitEvent(stream, wo.used, 0) != hipSuccess) {
+    *err = "hipStreamWaitEvent failed (dispatch-order buffers)";
+    return -3;
+  }
   size_t temp = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned*)nullptr, (unsigned*)nullptr,
                                          (const int*)nullptr, (int*)nullptr, (int)C) != hipSuccess) {
@@ -59,6 +63,10 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   }
   const size_t arr = ((size_t)C * 4 + 255) & ~(size_t)255;
   const size_t need = 4 * arr + temp;
+  if (!wo.used && hipEventCreateWithFlags(&wo.used, hipEventDisableTiming) != hipSuccess) {
+    *err = "hipEventCreate failed (dispatch-order buffers)";
+    return -3;
+  }
   if (need > wo.bytes) {
     if (wo.buf) (void)hipFree(wo.buf);
     wo.buf = nullptr;
@@ -83,6 +91,16 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   }
   *perm = iout;
   return 0;
+}
+
+void order_release(WorkOrder& wo) {
+  if (wo.buf) (void)hipFree(wo.buf);
+  if (wo.used) (void)hipEventDestroy(wo.used);
+  wo = WorkOrder{};
+}
+
+void order_mark_used(WorkOrder& wo, hipStream_t stream) {
+  if (wo.used && hipEventRecord(wo.used, stream) == hipSuccess) wo.pending = true;
 }
 
 }  // namespace mpct
