@@ -197,3 +197,34 @@ def test_vns_search_ranges(built, has_gpu):
     assert _rel(res.J1, ref["J1"]) < COST_RTOL
     assert _trel(res.u, ref["u"]) < TRAJ_RTOL
     assert _trel(res.uopt, ref["uopt"]) < TRAJ_RTOL
+
+
+def test_two_streams_share_a_scenario(env):
+    """Two device calls on one scenario, enqueued back to back on two streams without a host
+    sync: each launch reads its own heaviest-first permutation (work_order.hip), and the second
+    call's sort waits for the first launch before rewriting the shared buffer."""
+    import torch
+
+    from mpct.engine import eval_batch, eval_batch_device
+    from mpct.scenarios import candidate_grid
+
+    sc = env["sc"]
+    dev = torch.device("cuda", 0)
+    N2, Nu, d, l = candidate_grid(2048)
+    halves = [slice(0, 1024), slice(1024, 2048)]
+    ref = [eval_batch(sc, N2[h], Nu[h], d[h], l[h], env["r"][None]) for h in halves]
+    tr = torch.from_numpy(env["r"][None].copy()).to(dev)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = []
+    for h in halves:
+        t = [torch.from_numpy(np.ascontiguousarray(a[h])).to(dev) for a in (N2, Nu, d, l)]
+        out = dict(J1=torch.empty((1024, sc.my), dtype=torch.float64, device=dev),
+                   status=torch.empty(1024, dtype=torch.int32, device=dev),
+                   qp_iters=torch.empty(1024, dtype=torch.int64, device=dev))
+        outs.append((out, t))
+    torch.cuda.synchronize(dev)  # inputs resident; then the two launches are enqueued back to back
+    for (out, t), st in zip(outs, streams):
+        eval_batch_device(sc, *t, tr, out, stream=st)
+    torch.cuda.synchronize(dev)
+    for (out, _), rf in zip(outs, ref):
+        assert np.array_equal(out["J1"].cpu().numpy(), rf.J1)
