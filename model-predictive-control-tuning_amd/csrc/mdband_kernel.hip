@@ -38,6 +38,10 @@ struct BandLayout {
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
+#ifndef MPCT_BAND_CAPS_KB
+#define MPCT_BAND_CAPS_KB 26, 32, 40, 53, 80, 160  // LDS tiers of the class launches: 6/5/4/3/2/1 workgroups per CU
+                                               // (the last must be 160; tools/ab3.sh: 4 tiers 3.09 s, these 2.88 s)
+#endif
 #ifndef MPCT_BAND_STEP_L2
 #define MPCT_BAND_STEP_L2 1  // the QP reads the MV step table from global memory (L1/L2-resident, shared by every
                              // simulation) instead of an LDS copy: 21.5 KB less LDS at N2 = 127, 3.14 -> 3.09 s
@@ -857,12 +861,14 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
     return -4;
   }
   auto kern = mdband_closed_loop_kernel<MAXM>;
-  static const long long caps[4] = {40 * 1024, 53 * 1024, 80 * 1024, 160 * 1024};  // 4/3/2/1 per CU
-  long long lo[4], hi[4];
+  static const long long capkb[] = {MPCT_BAND_CAPS_KB};  // workgroups per CU: 160 KB / cap
+  constexpr int kCaps = (int)(sizeof(capkb) / sizeof(capkb[0]));
+  static_assert(kCaps <= 8, "at most 8 LDS tiers");
+  long long lo[8], hi[8];
   int ncls = 0;
-  for (long long l = 0; ncls < 4 && l < lds_max; ++ncls) {
+  for (long long l = 0; ncls < kCaps && l < lds_max; ++ncls) {
     lo[ncls] = l;
-    hi[ncls] = std::min(caps[ncls], lds_max);
+    hi[ncls] = std::min(capkb[ncls] * 1024, lds_max);
     l = hi[ncls];
   }
   for (int k = ncls - 1; k >= 0; --k) {
