@@ -631,6 +631,13 @@ __global__ void __launch_bounds__(64, 1)
 
 #include "work_order.h"
 
+#ifndef MPCT_NMPC_CAPS16_KB
+#define MPCT_NMPC_CAPS16_KB 13  // M <= 16 class: 12 workgroups per CU up to 13 KB, the rest above
+#endif
+#ifndef MPCT_NMPC_CAPS32_KB
+#define MPCT_NMPC_CAPS32_KB 32  // M <= 32 class: 5 workgroups per CU up to 32 KB, the rest above
+#endif
+
 namespace mpct {
 
 long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
@@ -645,10 +652,18 @@ static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int
                          const DevResult& out, FanScope& fs, int& nl, int mz_lo, bool& first, std::string* err) {
   const int Mhi = std::min(sc.nu * sc.numax, MAXM);
   const long long lds_max = nmpc_lds_bytes(Mhi, sc.n2max);
-  // 12 / 6 waves per CU for the small class, 5 / 2 for the large one
-  const long long cap = MAXM <= 16 ? 13 * 1024 : 32 * 1024;
-  const long long lo[2] = {0, cap}, hi[2] = {std::min(cap, lds_max), lds_max};
-  for (int k = (lds_max > cap ? 1 : 0); k >= 0; --k) {
+  // LDS tiers (KB) of the class launches; the last one takes the rest up to lds_max
+  static const long long c16[] = {MPCT_NMPC_CAPS16_KB}, c32[] = {MPCT_NMPC_CAPS32_KB};
+  const long long* caps = MAXM <= 16 ? c16 : c32;
+  const int ncap = MAXM <= 16 ? (int)(sizeof(c16) / sizeof(c16[0])) : (int)(sizeof(c32) / sizeof(c32[0]));
+  long long lo[8], hi[8];
+  int ncls = 0;
+  for (long long l = 0; ncls < 8 && l < lds_max; ++ncls) {
+    lo[ncls] = l;
+    hi[ncls] = ncls < ncap ? std::min(caps[ncls] * 1024, lds_max) : lds_max;
+    l = hi[ncls];
+  }
+  for (int k = ncls - 1; k >= 0; --k) {
     hipLaunchKernelGGL(nmpc_closed_loop_kernel<MAXM>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)hi[k],
                        fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, mz_lo, lo[k], hi[k],
                        first ? 1 : 0);
