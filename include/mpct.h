@@ -256,7 +256,11 @@ int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const in
 
 /* Same, all pointers DEVICE pointers (inputs already resident in HBM; results written to
  * device memory), enqueued on `stream` (a hipStream_t, NULL = default stream) and NOT
- * synchronised — the caller synchronises.  Used by multi-GPU sharding and the benchmark. */
+ * synchronised — the caller synchronises.  Used by multi-GPU sharding and the benchmark.
+ * Batches of 256 or more candidates are dispatched heaviest-first (an a-priori work key and a
+ * device radix sort on `stream`, ~20 us; results stay in the caller's order).  The sort buffers
+ * belong to the scenario.  Back-to-back calls on one scenario from different streams are safe:
+ * each sort waits for the launch that read the previous permutation. */
 int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
                                const double* delta, const double* lambda, int32_t nref,
                                const double* r, const double* v, const mpct_opts* opts,
