@@ -5,6 +5,7 @@ like MPCTuning.m:374-381.  Initial weights: the nlmpc object's delta = [1 1], la
 (VanDeVusse_NMPC.m:193-198).  python tools/tune_vandevusse.py [out.mat] [gam_max_iter]"""
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -18,7 +19,17 @@ out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "Va
 gmax = int(sys.argv[2]) if len(sys.argv) > 2 else 400
 sc, r, yref = vandevusse(n_max=31, nu_max=15)
 t0 = time.time()
+
+
+def _heartbeat():
+    # a GAM phase can run minutes without a log line: say so every minute
+    while True:
+        time.sleep(60)
+        print("... tuning, %.0f s" % (time.time() - t0), flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 N, Nu, delta, lam, Fob = mpc_tuning(sc, r, my=2, ny=2, w=VDV_W, nbp=5, nbc=4, dmin=np.zeros(2, dtype=int),
-                                    q0=np.array([1.0, 1.0]), w0=np.array([0.1, 0.1]), log=print, save_path=out,
+                                    q0=np.array([1.0, 1.0]), w0=np.array([0.1, 0.1]), log=lambda *a: print(*a, flush=True), save_path=out,
                                     gam_max_iter=gmax, lineal=False)
 print("N=%s Nu=%s delta=%s lambda=%s Fob=%s  (%.1f s)" % (N, Nu, delta, lam, Fob, time.time() - t0))
