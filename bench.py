@@ -338,16 +338,12 @@ def other_workload(args):
         cfg = {"workload": "VanDeVusse NMPC, N in 3..31, Nu in 2..15, nit=60 + open loop",
                "candidates_per_gpu": args.candidates}
     else:
-        from mpct.dtc import woodberry_mc
+        from mpct.dtc import config4_candidates, woodberry_mc
 
         D = 32
         sc, r, vv, _ = woodberry_mc(draws=D, n2_max=30, nu_max=10)
-        rng = np.random.default_rng(20250307)
         Cc = 10000
-        N2 = rng.integers(3, 31, Cc).astype(np.int32)
-        Nu = np.array([rng.integers(1, min(p, 10) + 1) for p in N2], dtype=np.int32)
-        l = 10.0 ** rng.uniform(-3, 1, (Cc, 2))
-        d = 10.0 ** rng.uniform(-3, 1, (Cc, 2))
+        N2, Nu, d, l = config4_candidates(Cc)
         refs, v, nref = r, vv, D
         w = np.ones(2)
         scaling, metric = "strong", "closed-loop DTC-GPC sims/sec (WoodBerry, 10,000 candidates x 32 draws)"

@@ -18,7 +18,9 @@
  *     it is reported in mpct_result.status[] with NaN costs (the reference swallows such
  *     errors with fprintf and continues: VNS2.m:161-163, GAM_fun.m:82-84).
  *   - threading: one scenario per host thread, or external synchronisation.  All device work
- *     of a call is complete when mpct_eval_batch returns.
+ *     of a call is complete when mpct_eval_batch returns.  A scenario keeps one context per GPU
+ *     it has been evaluated on (table copies, sort buffers, a library-owned stream); the
+ *     host-pointer entries synchronise that stream only, never the whole device.
  */
 #ifndef MPCT_H
 #define MPCT_H
@@ -29,7 +31,9 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 4 /* 4: nonlinear MPC scenarios (mpct_nmpc_scenario_create); 3: MD feed-forward +
+#define MPCT_ABI_VERSION 5 /* 5: one scenario on several GPUs of one process (mpct_eval_batch_multi,
+                              mpct_shard_range), kernel-instance query; the host-pointer entries wait on
+                              their own stream only.  4: nonlinear MPC scenarios (mpct_nmpc_scenario_create); 3: MD feed-forward +
                               soft output bands; 2: DTC-GPC predictor + plant-only disturbances + plant
                               variants; v1..v3 descriptors accepted */
 
@@ -265,6 +269,30 @@ int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, c
                                const double* delta, const double* lambda, int32_t nref,
                                const double* r, const double* v, const mpct_opts* opts,
                                mpct_result* out, void* stream);
+
+/* Score C candidates on ndev GPUs of this process at once (host pointers, like mpct_eval_batch).
+ * The candidates are independent (VNS2.m:148-169, GAM_fun.m:79-91 score each one in isolation),
+ * so they are split into contiguous shards [k*ceil(C/ndev), (k+1)*ceil(C/ndev)) (mpct_shard_range),
+ * shard k on devices[k]; each device gets its own copy of the scenario tables and its own stream,
+ * one host thread per device drives its H2D copies, launch and D2H copies, and the call returns
+ * when every shard is done.  Results land in the caller's order (simulation s = c*nref + k), so a
+ * single-threaded MATLAB host drives all GPUs of a node with one call.  ndev = 1 is exactly
+ * mpct_eval_batch on devices[0].  opts->device is ignored.  Errors: the first failing device's
+ * code, its message prefixed with "device <ordinal>: ". */
+int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const int32_t* devices, int64_t C,
+                              const int32_t* N2, const int32_t* Nu, const double* delta, const double* lambda,
+                              int32_t nref, const double* r, const double* v, const mpct_opts* opts,
+                              mpct_result* out);
+
+/* The contiguous shard [*lo, *hi) of C candidates that device slot k of ndev scores (the split of
+ * mpct_eval_batch_multi and of the torch.distributed ranks).  Returns *hi - *lo, or <0. */
+int64_t mpct_shard_range(int64_t C, int32_t ndev, int32_t k, int64_t* lo, int64_t* hi);
+
+/* Name of the kernel instance mpct_eval_batch(_device) launches for this scenario and options,
+ * e.g. "gpc_closed_loop_kernel<16,false,false>" (QP-size class, DTC mode, open-loop/trajectory
+ * state).  Copies at most cap-1 characters plus a NUL into buf; returns the name's length, or <0.
+ * No device needed (tests pin the instance a benchmark times). */
+int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts* opts, char* buf, int32_t cap);
 
 /* Bytes of dynamic LDS one simulation's workgroup uses for this scenario at (N2, Nu); <0 on
  * error.  Lets a host check occupancy before launching. */

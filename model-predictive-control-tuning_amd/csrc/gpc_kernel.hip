@@ -877,6 +877,12 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
   return 0;
 }
 
+// the instance launch_closed_loop picks (mpct_kernel_instance): QP size class, DTC, EXT
+std::string closed_loop_instance(int maxM, bool dtc, bool ext) {
+  const int cls = maxM <= 16 ? 16 : maxM <= 32 ? 32 : 64;
+  return "gpc_closed_loop_kernel<" + std::to_string(cls) + (dtc ? ",true" : ",false") + (ext ? ",true>" : ",false>");
+}
+
 int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                        const double* delta, const double* lambda, const double* r,
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 #include <cstdio>
+#include <thread>
 
 #include "../../include/mpct.h"
 #include "launch_fan.h"
@@ -29,6 +30,7 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
                        WorkOrder* wo, hipStream_t stream, std::string* err);
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
+std::string closed_loop_instance(int maxM, bool dtc, bool ext);
 // defined in mdband_kernel.hip
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
@@ -42,6 +44,20 @@ long long nmpc_lds_bytes(int M, int N);
 }  // namespace mpct
 
 using namespace mpct;
+
+// Everything a scenario keeps on one device.  The host-pointer entries run on the library-owned
+// stream `stream` and synchronise only it (not the device), so other streams, host threads and
+// the contexts of other devices proceed concurrently.
+struct DevCtx {
+  int dev = -1;
+  void* dtab = nullptr;  // the scenario's tables, one 256-B-aligned blob
+  DevScenario ds{};
+  void* dscratch = nullptr;  // host-API input/result buffers (grow only)
+  size_t dscratch_bytes = 0;
+  hipStream_t stream = nullptr;
+  LaunchFan fan;    // auxiliary streams of the class launches (band / NMPC kernels)
+  WorkOrder order;  // dispatch-order sort buffers (GPC and NMPC kernels)
+};
 
 static thread_local std::string g_err;
 
@@ -84,15 +100,9 @@ struct mpct_scenario {
   double ts = 0.0, sqp_tol = 1e-8;
   std::vector<int> xc;      // [ny] 0-based output states
   std::vector<double> nm;   // see DevScenario::nm
-  // device state
-  int dev = -2;
-  void* dtab = nullptr;
-  DevScenario ds{};
-  // scratch buffers for the host-pointer API (grow only)
-  void* dscratch = nullptr;
-  LaunchFan fan;  // auxiliary streams of the class launches (band / NMPC kernels)
-  WorkOrder order;  // dispatch-order sort buffers (GPC and NMPC kernels)
-  size_t dscratch_bytes = 0;
+  // device state, one context per device ordinal (created on first use, kept until destroy):
+  // a scenario can be evaluated on several GPUs of one process (mpct_eval_batch_multi)
+  std::vector<DevCtx*> ctx;
 };
 
 extern "C" int32_t mpct_abi_version(void) { return MPCT_ABI_VERSION; }
@@ -603,15 +613,21 @@ extern "C" int32_t mpct_nmpc_scenario_create(const mpct_nmpc_desc* d, mpct_scena
 
 extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
   if (!s) return;
-  if (s->dtab || s->dscratch) {
-    int cur = -1;
-    if (hipGetDevice(&cur) == hipSuccess && s->dev >= 0) (void)hipSetDevice(s->dev);
-    if (s->dtab) (void)hipFree(s->dtab);
-    if (s->dscratch) (void)hipFree(s->dscratch);
-    order_release(s->order);
-    s->fan.release();
-    if (cur >= 0) (void)hipSetDevice(cur);
+  int cur = -1;
+  const bool any = std::any_of(s->ctx.begin(), s->ctx.end(), [](DevCtx* c) { return c != nullptr; });
+  if (any && hipGetDevice(&cur) != hipSuccess) cur = -1;
+  for (DevCtx* c : s->ctx) {
+    if (!c) continue;
+    (void)hipSetDevice(c->dev);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->dtab) (void)hipFree(c->dtab);
+    if (c->dscratch) (void)hipFree(c->dscratch);
+    order_release(c->order);
+    c->fan.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
   }
+  if (cur >= 0) (void)hipSetDevice(cur);
   delete s;
 }
 
@@ -656,7 +672,9 @@ static void compact_taps(const mpct_scenario* s, DevScenario& ds) {
   ds.mz_maxbc = mb;
 }
 
-static int ensure_device(mpct_scenario* s, int want_dev) {
+// the context of device want_dev (-1: the calling thread's current device), created and its
+// tables uploaded on first use; makes that device current for the calling thread
+static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out) {
   int dev = want_dev;
   if (dev < 0) {
     if (hipGetDevice(&dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
@@ -665,17 +683,11 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) return fail(MPCT_EDEVICE, "no HIP device");
   if (dev >= cnt) return fail(MPCT_EINVAL, "device ordinal out of range");
   if (hipSetDevice(dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipSetDevice failed");
-  if (s->dev == dev && s->dtab) return MPCT_OK;
-  if (s->dtab) {
-    (void)hipFree(s->dtab);
-    s->dtab = nullptr;
+  if ((int)s->ctx.size() < cnt) s->ctx.resize(cnt, nullptr);
+  if (s->ctx[dev]) {
+    *out = s->ctx[dev];
+    return MPCT_OK;
   }
-  if (s->dscratch) {
-    (void)hipFree(s->dscratch);
-    s->dscratch = nullptr;
-    s->dscratch_bytes = 0;
-  }
-  order_release(s->order);
   // pack all tables into one allocation, 256-B aligned pieces
   std::vector<char> blob;
   auto put = [&](const void* p, size_t bytes) -> size_t {
@@ -717,8 +729,14 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
     (void)hipFree(dp);
     return fail(MPCT_EDEVICE, "hipMemcpy(tables) failed");
   }
+  DevCtx* cx = new DevCtx();
+  if (hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipFree(dp);
+    delete cx;
+    return fail(MPCT_EDEVICE, "hipStreamCreate failed");
+  }
   char* b = static_cast<char*>(dp);
-  DevScenario& ds = s->ds;
+  DevScenario& ds = cx->ds;
   ds.my = s->my;
   ds.nu = s->nu;
   ds.nd = s->nd + s->nq;  // ring-fed plant inputs (their signals are v's rows)
@@ -776,9 +794,11 @@ static int ensure_device(mpct_scenario* s, int want_dev) {
   ds.sqp_tol = s->sqp_tol;
   ds.xc = reinterpret_cast<const int*>(b + o_xc);
   ds.nm = reinterpret_cast<const double*>(b + o_nm);
-  s->dtab = dp;
-  s->dev = dev;
-  if ((s->mdband || s->nmpc) && !s->fan.init(dev)) s->fan.release();  // no fan: one stream, still correct
+  cx->dtab = dp;
+  cx->dev = dev;
+  if ((s->mdband || s->nmpc) && !cx->fan.init(dev)) cx->fan.release();  // no fan: one stream, still correct
+  s->ctx[dev] = cx;
+  *out = cx;
   return MPCT_OK;
 }
 
@@ -801,16 +821,10 @@ static int check_args(mpct_scenario* s, int64_t C, int32_t nref, const int32_t* 
   return MPCT_OK;
 }
 
-extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
-                                          const double* delta, const double* lambda, int32_t nref,
-                                          const double* r, const double* v, const mpct_opts* opts,
-                                          mpct_result* out, void* stream) {
-  int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
-  if (rc) return rc;
-  if (!out) return fail(MPCT_EINVAL, "null result");
-  rc = ensure_device(s, opts ? opts->device : -1);
-  if (rc) return rc;
-  if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
+// enqueue one batch with device pointers on `stream` (ctx's device is current)
+static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* N2, const int32_t* Nu,
+                        const double* delta, const double* lambda, int32_t nref, const double* r, const double* v,
+                        const mpct_opts* opts, const mpct_result* out, hipStream_t stream) {
   if (C == 0) return MPCT_OK;
   DevOpts dop = make_opts(opts);
   DevResult dr{out->J1, out->j21, out->j22, out->Jnu, out->status, out->qp_iters,
@@ -823,20 +837,19 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   dr.prof = dprof;
 #endif
   std::string err;
+  int rc;
   if (s->nmpc)
-    rc = launch_nmpc(s->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, static_cast<hipStream_t>(stream), &s->fan,
-                     &s->order, &err);
+    rc = launch_nmpc(cx->ds, C, nref, N2, Nu, delta, lambda, r, dop, dr, stream, &cx->fan, &cx->order, &err);
   else if (s->mdband)
-    rc = launch_mdband(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, static_cast<hipStream_t>(stream),
-                       &s->fan, &err);
+    rc = launch_mdband(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, stream, &cx->fan, &err);
   else
-    rc = launch_closed_loop(s->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &s->order,
-                            static_cast<hipStream_t>(stream), &err);
+    rc = launch_closed_loop(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &cx->order,
+                            stream, &err);
   if (rc) return fail(rc, err);
 #ifdef MPCT_PROFILE
   {
     std::vector<unsigned long long> hp(S * PROF_N);
-    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    (void)hipStreamSynchronize(stream);
     (void)hipMemcpy(hp.data(), dprof, sizeof(unsigned long long) * S * PROF_N, hipMemcpyDeviceToHost);
     (void)hipFree(dprof);
     double sum[PROF_N] = {0}, mx[PROF_N] = {0};
@@ -855,19 +868,32 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   return MPCT_OK;
 }
 
-extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
-                                   const double* delta, const double* lambda, int32_t nref, const double* r,
-                                   const double* v, const mpct_opts* opts, mpct_result* out) {
+extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                                          const double* delta, const double* lambda, int32_t nref,
+                                          const double* r, const double* v, const mpct_opts* opts,
+                                          mpct_result* out, void* stream) {
   int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
   if (rc) return rc;
   if (!out) return fail(MPCT_EINVAL, "null result");
-  rc = ensure_device(s, opts ? opts->device : -1);
+  if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
+  DevCtx* cx = nullptr;
+  rc = device_ctx(s, opts ? opts->device : -1, &cx);
   if (rc) return rc;
+  return launch_batch(s, cx, C, N2, Nu, delta, lambda, nref, r, v, opts, out, static_cast<hipStream_t>(stream));
+}
+
+// host buffers in, host buffers out, on the context's own stream: H2D of the candidates and
+// signals, the launch, D2H of the results, then a wait on that stream only
+static int eval_host(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* N2, const int32_t* Nu,
+                     const double* delta, const double* lambda, int32_t nref, const double* r, const double* v,
+                     const mpct_opts* opts, mpct_result* out) {
+  if (hipSetDevice(cx->dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipSetDevice failed");
   if (C == 0) return MPCT_OK;
   const int my = s->my, nu = s->nu, nd = s->nd, nit = s->nit;
   const int64_t S = C * nref;
   const bool traj = opts && opts->want_traj;
   const bool ol = opts && opts->open_loop;
+  hipStream_t st = cx->stream;
   // device scratch layout
   size_t off = 0;
   auto slot = [&](size_t bytes) {
@@ -881,21 +907,24 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
   size_t o_st = slot(S * 4), o_it = slot(S * 8);
   size_t o_y = traj ? slot(S * my * nit * 8) : 0, o_u = traj ? slot(S * nu * nit * 8) : 0;
   size_t o_ys = (traj && ol) ? slot(S * my * nit * 8) : 0, o_uo = (traj && ol) ? slot(S * nu * nit * 8) : 0;
-  if (off > s->dscratch_bytes) {
-    if (s->dscratch) (void)hipFree(s->dscratch);
-    s->dscratch = nullptr;
-    s->dscratch_bytes = 0;
-    if (hipMalloc(&s->dscratch, off) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(scratch) failed");
-    s->dscratch_bytes = off;
+  if (off > cx->dscratch_bytes) {
+    if (cx->dscratch) {
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(cx->dscratch);
+    }
+    cx->dscratch = nullptr;
+    cx->dscratch_bytes = 0;
+    if (hipMalloc(&cx->dscratch, off) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(scratch) failed");
+    cx->dscratch_bytes = off;
   }
-  char* b = static_cast<char*>(s->dscratch);
+  char* b = static_cast<char*>(cx->dscratch);
   auto h2d = [&](size_t o, const void* p, size_t bytes) {
-    return bytes == 0 || hipMemcpy(b + o, p, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    return bytes == 0 || hipMemcpyAsync(b + o, p, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
   };
   if (!h2d(o_N2, N2, C * 4) || !h2d(o_Nu, Nu, C * 4) || !h2d(o_d, delta, C * my * 8) ||
       !h2d(o_l, lambda, C * nu * 8) || !h2d(o_r, r, (size_t)nref * my * nit * 8) ||
       (nd + s->nq > 0 && !h2d(o_v, v, (size_t)nref * (nd + s->nq) * nit * 8)))
-    return fail(MPCT_EDEVICE, "hipMemcpy(inputs) failed");
+    return fail(MPCT_EDEVICE, "hipMemcpyAsync(inputs) failed");
   mpct_result dres{};
   dres.J1 = reinterpret_cast<double*>(b + o_J1);
   dres.j21 = reinterpret_cast<double*>(b + o_j21);
@@ -911,17 +940,16 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
       dres.uopt = reinterpret_cast<double*>(b + o_uo);
     }
   }
-  rc = mpct_eval_batch_device(s, C, reinterpret_cast<const int32_t*>(b + o_N2),
-                              reinterpret_cast<const int32_t*>(b + o_Nu),
-                              reinterpret_cast<const double*>(b + o_d),
-                              reinterpret_cast<const double*>(b + o_l), nref,
-                              reinterpret_cast<const double*>(b + o_r),
-                              nd + s->nq > 0 ? reinterpret_cast<const double*>(b + o_v) : nullptr, opts, &dres,
-                              nullptr);
-  if (rc) return rc;
-  if (hipDeviceSynchronize() != hipSuccess) return fail(MPCT_EDEVICE, "kernel execution failed");
+  int rc = launch_batch(s, cx, C, reinterpret_cast<const int32_t*>(b + o_N2), reinterpret_cast<const int32_t*>(b + o_Nu),
+                        reinterpret_cast<const double*>(b + o_d), reinterpret_cast<const double*>(b + o_l), nref,
+                        reinterpret_cast<const double*>(b + o_r),
+                        nd + s->nq > 0 ? reinterpret_cast<const double*>(b + o_v) : nullptr, opts, &dres, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
   auto d2h = [&](void* dst, const void* src, size_t bytes) {
-    return !dst || bytes == 0 || hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+    return !dst || bytes == 0 || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
   };
   bool ok = d2h(out->J1, dres.J1, S * my * 8) && d2h(out->j21, dres.j21, S * my * 8) &&
             d2h(out->j22, dres.j22, S * my * 8) && d2h(out->Jnu, dres.Jnu, S * nu * 8) &&
@@ -930,8 +958,116 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
     ok = ok && d2h(out->y, dres.y, S * my * nit * 8) && d2h(out->u, dres.u, S * nu * nit * 8);
     if (ol) ok = ok && d2h(out->ys, dres.ys, S * my * nit * 8) && d2h(out->uopt, dres.uopt, S * nu * nit * 8);
   }
-  if (!ok) return fail(MPCT_EDEVICE, "hipMemcpy(results) failed");
+  const hipError_t se = hipStreamSynchronize(st);
+  if (se != hipSuccess) return fail(MPCT_EDEVICE, std::string("kernel execution failed: ") + hipGetErrorString(se));
+  if (!ok) return fail(MPCT_EDEVICE, "hipMemcpyAsync(results) failed");
   return MPCT_OK;
+}
+
+extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N2, const int32_t* Nu,
+                                   const double* delta, const double* lambda, int32_t nref, const double* r,
+                                   const double* v, const mpct_opts* opts, mpct_result* out) {
+  int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
+  if (rc) return rc;
+  if (!out) return fail(MPCT_EINVAL, "null result");
+  if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
+  DevCtx* cx = nullptr;
+  rc = device_ctx(s, opts ? opts->device : -1, &cx);
+  if (rc) return rc;
+  return eval_host(s, cx, C, N2, Nu, delta, lambda, nref, r, v, opts, out);
+}
+
+// result pointer of simulation s0 onwards (row-major per simulation), NULL stays NULL
+template <class T>
+static T* at(T* p, int64_t s0, int64_t width) {
+  return p ? p + s0 * width : nullptr;
+}
+
+extern "C" int64_t mpct_shard_range(int64_t C, int32_t ndev, int32_t k, int64_t* lo, int64_t* hi) {
+  if (C < 0 || ndev < 1 || k < 0 || k >= ndev || !lo || !hi) return fail(MPCT_EINVAL, "bad shard arguments");
+  const int64_t per = (C + ndev - 1) / ndev;
+  *lo = std::min<int64_t>(C, per * k);
+  *hi = std::min<int64_t>(C, per * (k + 1));
+  return *hi - *lo;
+}
+
+extern "C" int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const int32_t* devices, int64_t C,
+                                         const int32_t* N2, const int32_t* Nu, const double* delta,
+                                         const double* lambda, int32_t nref, const double* r, const double* v,
+                                         const mpct_opts* opts, mpct_result* out) {
+  int rc = check_args(s, C, nref, N2, Nu, delta, lambda, r, v);
+  if (rc) return rc;
+  if (!out) return fail(MPCT_EINVAL, "null result");
+  if (ndev < 1 || ndev > 64 || !devices) return fail(MPCT_EINVAL, "ndev must be 1..64 with a device list");
+  if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
+  for (int a = 0; a < ndev; ++a)
+    for (int b2 = a + 1; b2 < ndev; ++b2)
+      if (devices[a] == devices[b2]) return fail(MPCT_EINVAL, "duplicate device in the list");
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
+  // contexts (table uploads) serially on this thread, before any worker starts
+  std::vector<DevCtx*> cxs(ndev, nullptr);
+  for (int k = 0; k < ndev; ++k) {
+    if (devices[k] < 0) return fail(MPCT_EINVAL, "device ordinals must be >= 0");
+    rc = device_ctx(s, devices[k], &cxs[k]);
+    if (rc) {
+      (void)hipSetDevice(cur);
+      return rc;
+    }
+  }
+  const int my = s->my, nu = s->nu, nin = s->nd + s->nq, nit = s->nit;
+  (void)nin;
+  std::vector<int> rcs(ndev, MPCT_OK);
+  std::vector<std::string> errs(ndev);
+  auto shard = [&](int k) {
+    int64_t lo = 0, hi = 0;
+    mpct_shard_range(C, ndev, k, &lo, &hi);
+    if (hi <= lo) return;
+    const int64_t s0 = lo * nref;  // simulations of candidate lo onwards (s = c*nref + kref)
+    mpct_result o{};
+    o.J1 = at(out->J1, s0, my);
+    o.j21 = at(out->j21, s0, my);
+    o.j22 = at(out->j22, s0, my);
+    o.Jnu = at(out->Jnu, s0, nu);
+    o.status = at(out->status, s0, 1);
+    o.qp_iters = at(out->qp_iters, s0, 1);
+    o.y = at(out->y, s0, (int64_t)my * nit);
+    o.u = at(out->u, s0, (int64_t)nu * nit);
+    o.ys = at(out->ys, s0, (int64_t)my * nit);
+    o.uopt = at(out->uopt, s0, (int64_t)nu * nit);
+    rcs[k] = eval_host(s, cxs[k], hi - lo, N2 + lo, Nu + lo, delta + lo * my, lambda + lo * nu, nref, r, v, opts, &o);
+    if (rcs[k]) errs[k] = g_err;  // g_err is thread-local: carry it to the caller
+  };
+  if (ndev == 1) {
+    shard(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int k = 1; k < ndev; ++k) th.emplace_back(shard, k);
+    shard(0);
+    for (auto& t : th) t.join();
+  }
+  (void)hipSetDevice(cur);
+  for (int k = 0; k < ndev; ++k)
+    if (rcs[k]) return fail(rcs[k], "device " + std::to_string(devices[k]) + ": " + errs[k]);
+  return MPCT_OK;
+}
+
+extern "C" int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts* opts, char* buf, int32_t cap) {
+  if (!s) return fail(MPCT_EINVAL, "null scenario");
+  std::string nm;
+  const bool ext = opts && (opts->open_loop || opts->want_traj);
+  if (s->nmpc)
+    nm = "nmpc_closed_loop_kernel (QP-size x LDS-tier class launches)";
+  else if (s->mdband)
+    nm = "mdband_closed_loop_kernel (QP-size x LDS-tier class launches)";
+  else
+    nm = closed_loop_instance(s->nu * s->numax, s->dtc != 0, ext);
+  if (buf && cap > 0) {
+    const size_t n = std::min<size_t>(nm.size(), (size_t)cap - 1);
+    std::memcpy(buf, nm.data(), n);
+    buf[n] = '\0';
+  }
+  return (int32_t)nm.size();
 }
 
 extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {

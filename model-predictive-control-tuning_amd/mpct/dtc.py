@@ -120,6 +120,18 @@ def woodberry_mc_plants(draws: int, seed: int = 20250307, gain_spread: float = 0
     return out
 
 
+def config4_candidates(C: int = 10000, seed: int = 20250307, p_max: int = 30, m_max: int = 10):
+    """SURVEY §8d config 4 candidate grid: p in 3..p_max, m in 1..min(p, m_max), then log10 lambda
+    and log10 delta ~ U(-3, 1), numpy default_rng(seed) in that order.  Returns (N2, Nu, delta,
+    lambda) in the engine's candidate layout (one p / m for both loops: the toolbox-style max)."""
+    rng = np.random.default_rng(seed)
+    N2 = rng.integers(3, p_max + 1, C).astype(np.int32)
+    Nu = np.array([rng.integers(1, min(int(p), m_max) + 1) for p in N2], dtype=np.int32)
+    lam = 10.0 ** rng.uniform(-3, 1, (C, 2))
+    delta = 10.0 ** rng.uniform(-3, 1, (C, 2))
+    return N2, Nu, delta, lam
+
+
 def woodberry_mc(draws: int = 32, n2_max: int = 30, nu_max: int = 10, nit: int = 200, seed: int = 20250307,
                  alfa: float = 0.7, raio: float = 0.8):
     """Config 4 scenario: the DTC-GPC of woodberry_dtc evaluated over `draws` mismatched plants

@@ -301,3 +301,61 @@ def closedloop_toolbox(sc: Scenario, r, v, N, Nu, delta, lam, nit=None):
                      open_loop=True, want_traj=True)
     t = np.arange(nit) * sc.Ts
     return res.y[0], res.u[0], t, res.ys[0], res.uopt[0]
+
+
+def kernel_instance(sc: Scenario, open_loop=False, want_traj=False) -> str:
+    """mpct_kernel_instance: the kernel instance eval_batch launches for these options."""
+    buf = C.create_string_buffer(128)
+    n = sc.lib.mpct_kernel_instance(sc.handle, C.byref(_opts(open_loop, want_traj)), buf, len(buf))
+    if n < 0:
+        raise MpctError(_lib.last_error())
+    return buf.value.decode()
+
+
+def shard_range(C_: int, ndev: int, k: int):
+    """mpct_shard_range: the contiguous candidate shard [lo, hi) of device slot k."""
+    lo, hi = C.c_int64(), C.c_int64()
+    if _lib.load().mpct_shard_range(int(C_), int(ndev), int(k), C.byref(lo), C.byref(hi)) < 0:
+        raise MpctError(_lib.last_error())
+    return lo.value, hi.value
+
+
+def eval_batch_multi(sc: Scenario, devices, N2, Nu, delta, lam, refs, v=None, open_loop=False,
+                     want_traj=False, max_qp_iter=0, feas_tol=0.0) -> EvalResult:
+    """mpct_eval_batch_multi: one call scores the candidates on every GPU of ``devices`` at once
+    (contiguous shards, one host thread and stream per device, results in the caller's order)."""
+    devs = np.ascontiguousarray(np.atleast_1d(devices), dtype=np.int32)
+    N2 = np.ascontiguousarray(np.atleast_1d(N2), dtype=np.int32)
+    Cn = N2.size
+    Nu = np.ascontiguousarray(np.broadcast_to(np.atleast_1d(Nu), (Cn,)), dtype=np.int32)
+    delta = np.ascontiguousarray(np.asarray(delta, dtype=float).reshape(Cn, sc.my))
+    lam = np.ascontiguousarray(np.asarray(lam, dtype=float).reshape(Cn, sc.nu))
+    refs = np.ascontiguousarray(np.asarray(refs, dtype=float).reshape(-1, sc.my, sc.nit))
+    nref = refs.shape[0]
+    S = Cn * nref
+    vv = None
+    if sc.nd + sc.nq:
+        vv = np.ascontiguousarray(np.broadcast_to(np.asarray(v, dtype=float).reshape(-1, sc.nd + sc.nq, sc.nit),
+                                                  (nref, sc.nd + sc.nq, sc.nit)))
+    res = EvalResult(J1=np.zeros((S, sc.my)), j21=np.zeros((S, sc.my)), j22=np.zeros((S, sc.my)),
+                     Jnu=np.zeros((S, sc.nu)), status=np.zeros(S, dtype=np.int32),
+                     qp_iters=np.zeros(S, dtype=np.int64), nref=nref)
+    r = _lib.MpctResult()
+    r.J1, r.j21, r.j22, r.Jnu = _dp(res.J1), _dp(res.j21), _dp(res.j22), _dp(res.Jnu)
+    r.status = _ip(res.status)
+    r.qp_iters = res.qp_iters.ctypes.data_as(_lib.c_int64_p)
+    if want_traj:
+        res.y = np.zeros((S, sc.my, sc.nit))
+        res.u = np.zeros((S, sc.nu, sc.nit))
+        r.y, r.u = _dp(res.y), _dp(res.u)
+        if open_loop:
+            res.ys = np.zeros((S, sc.my, sc.nit))
+            res.uopt = np.zeros((S, sc.nu, sc.nit))
+            r.ys, r.uopt = _dp(res.ys), _dp(res.uopt)
+    o = _opts(open_loop, want_traj, -1, max_qp_iter, feas_tol)
+    rc = sc.lib.mpct_eval_batch_multi(sc.handle, len(devs), _ip(devs), Cn, N2.ctypes.data, Nu.ctypes.data,
+                                      delta.ctypes.data, lam.ctypes.data, nref, refs.ctypes.data,
+                                      vv.ctypes.data if vv is not None else None, C.byref(o), C.byref(r))
+    if rc != 0:
+        raise MpctError("mpct_eval_batch_multi failed (%d): %s" % (rc, _lib.last_error()))
+    return res

@@ -337,19 +337,45 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
 
 
 # --------------------------------------------------------------------------------------------
-def save_tuning_parameters(path: str, N, Nu, delta, lam, scale: dict | None = None, date: str | None = None):
-    """MPCTuning.m:374-381 Tuning_Parameters {N, Nu, delta, lambda, scale.{L,R,Ru,Rv}, date}
-    (the mpc object itself is MATLAB-only and is not written).  '.mat' -> MAT v5 via scipy,
-    anything else -> JSON.  The struct reads back with the drivers' tuning=false path
-    (Shell3x3.m:169-185: Tuning_Parameters.N / .Nu / .delta / .lambda)."""
+def scale_record(L, R, nu: int) -> dict:
+    """Tuning_Parameters.scale as MPCTuning.m:154-160 builds it: L, R (diagonal CondMin scalings),
+    Ru = R(1:ny,1:ny) for the MVs, Rv = R(ny+1:end,ny+1:end) for the measured disturbances (empty
+    when there are none); the drivers' resume path reads all four (Shell3x3.m:180-183)."""
+    L = np.diag(np.asarray(L, dtype=float).ravel()) if np.ndim(L) < 2 else np.asarray(L, dtype=float)
+    R = np.diag(np.asarray(R, dtype=float).ravel()) if np.ndim(R) < 2 else np.asarray(R, dtype=float)
+    return {"L": L, "R": R, "Ru": R[:nu, :nu], "Rv": R[nu:, nu:]}
+
+
+def matlab_datenum(t) -> float:
+    """MATLAB datenum of a datetime (days since year 0; datenum(1970,1,1) = 719529)."""
     import datetime
 
-    rec = {"N": int(np.max(N)), "Nu": np.asarray(Nu, dtype=float).reshape(1, -1),
+    epoch = datetime.datetime(1970, 1, 1)
+    return 719529.0 + (t - epoch).total_seconds() / 86400.0
+
+
+def save_tuning_parameters(path: str, N, Nu, delta, lam, scale: dict | None = None, date=None):
+    """MPCTuning.m:374-381 Tuning_Parameters {N, Nu, delta, lambda, scale.{L,R,Ru,Rv}, date}.
+    ``scale``: scale_record(L, R, nu) (a dict holding only L and R is completed with Ru, Rv from
+    R's leading nu x nu block: MPCTuning.m:156-157).  ``date``: MATLAB's datetime object cannot be
+    written outside MATLAB, so it is stored as its datenum (double; datetime(date,
+    'ConvertFrom','datenum') restores it) plus date_str.  The mpc object (Tuning_Parameters.mpcobj)
+    is MATLAB-only: the MATLAB host attaches it (matlab/mpct_tuning_record.m).  '.mat' -> MAT v5 via
+    scipy, anything else -> JSON.  The drivers' tuning=false path reads N / Nu / delta / lambda /
+    scale.{L,R,Ru,Rv} back (Shell3x3.m:176-183)."""
+    import datetime
+
+    now = date or datetime.datetime.now()
+    Nu_ = np.asarray(Nu, dtype=float).reshape(1, -1)
+    rec = {"N": int(np.max(N)), "Nu": Nu_,
            "delta": np.asarray(delta, dtype=float).reshape(1, -1),
            "lambda": np.asarray(lam, dtype=float).reshape(1, -1),
-           "date": date or datetime.datetime.now().strftime("%d-%b-%Y %H:%M:%S")}
+           "date": matlab_datenum(now), "date_str": now.strftime("%d-%b-%Y %H:%M:%S")}
     if scale is not None:
-        rec["scale"] = {k: np.asarray(v, dtype=float) for k, v in scale.items()}
+        sc = {k: np.asarray(v, dtype=float) for k, v in scale.items()}
+        if "R" in sc and ("Ru" not in sc or "Rv" not in sc):
+            sc = scale_record(sc["L"], sc["R"], Nu_.size)
+        rec["scale"] = sc
     if path.endswith(".mat"):
         from scipy.io import savemat
 
@@ -368,17 +394,21 @@ def save_tuning_parameters(path: str, N, Nu, delta, lam, scale: dict | None = No
 
 
 # --------------------------------------------------------------------------------------------
-def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None):
+def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None, mdv=None):
     """Batched evaluators over the HIP engine (one eval_batch call per batch):
       batch_j1(X rows)                 -> J1 rows  (GAM_fun.m:55-116 with Par.N / Par.Nu, which
                                           closedloop_toolbox reduces with max, :36-40)
       batch_vns(keys, delta, lambda)   -> F per (N, Nu) neighbour (VNS2.m:147-195: my step
-                                          simulations for square plants, F = sum(j21 + j22) +
-                                          N(1) + sum(Jnu)); failed simulations score NaN."""
+                                          simulations for square plants, one simulation with Xsp
+                                          for non-square ones, F = sum(j21 + j22) + N(1) + sum(Jnu)).
+    mdv = Par.mdv (nd x nit, already scaled by Rv, MPCTuning.m:191) reaches every simulation
+    (GAM_fun.m:81, VNS2.m:153,168).  Only fatal statuses (objectives.FATAL_STATUS: the reference's
+    sim would have thrown) score NaN; iteration caps keep their finite cost."""
     from .engine import eval_batch
-    from .objectives import vns_objective
+    from .objectives import failed, vns_objective
 
     my, ny = par.my, par.ny
+    v = None if mdv is None or np.size(mdv) == 0 else np.asarray(mdv, dtype=float)[None]
 
     def batch_j1(X):
         X = np.atleast_2d(np.asarray(X, dtype=float))
@@ -388,9 +418,9 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None):
         lam = np.abs(X[:, my:my + ny])
         N2 = np.full(C, int(np.max(par.N)), dtype=np.int32)
         Nu = np.full(C, int(np.max(par.Nu)), dtype=np.int32)
-        res = eval_batch(sc, N2, Nu, delta, lam, np.asarray(r)[None], device=device)
+        res = eval_batch(sc, N2, Nu, delta, lam, np.asarray(r)[None], v=v, device=device)
         J1 = res.J1.copy()
-        J1[res.status != 0] = np.nan
+        J1[failed(res.status)] = np.nan
         return J1
 
     def batch_vns(keys, delta, lam):
@@ -399,16 +429,16 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None):
         Nu = np.array([max(k[1]) for k in keys], dtype=np.int32)
         d = np.tile(np.asarray(delta, dtype=float), (C, 1))
         l = np.tile(np.asarray(lam, dtype=float), (C, 1))
-        F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device, refs=vns_refs)
-        ok = res.status.reshape(C, -1).max(axis=1) == 0
-        return np.where(ok, F, np.nan)
+        F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device, refs=vns_refs, mdv=mdv)
+        bad = failed(res.status).reshape(C, -1).any(axis=1)
+        return np.where(bad, np.nan, F)
 
     return batch_j1, batch_vns
 
 
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
-               gam_max_iter: int = 400, lineal: bool = True):
+               gam_max_iter: int = 400, lineal: bool = True, mdv=None):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
@@ -422,8 +452,9 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
     if not lineal:
         from .objectives import vns_refs_nonlinear
 
-        vns_refs = vns_refs_nonlinear(r)
-    batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device, vns_refs=vns_refs)
+        # square: Xsp.*sel one output at a time (VNS2.m:148-155); non-square: Xsp whole (:168)
+        vns_refs = vns_refs_nonlinear(r) if my == ny else np.asarray(r, dtype=float)[None]
+    batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device, vns_refs=vns_refs, mdv=mdv)
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
                                                   gam_max_iter=gam_max_iter)
     if save_path:

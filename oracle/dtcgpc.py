@@ -345,13 +345,38 @@ def woodberry_models(deltak: float = 0.0, deltaL: float = 0.0, Ts: float = 1.0):
     return P, Pn, Pq
 
 
+def woodberry_mc_draws(draws: int, seed: int = 20250307, gain_spread: float = 0.2, max_dshift: int = 2,
+                       Ts: float = 1.0):
+    """SURVEY §8d config 4 plant-mismatch draws, modelled on DTC_GPC_WW.m:18-19 (P = Pn with the
+    gain scaled by 1 + deltak and the delay shifted by deltaL), one draw per entry: gain x
+    (1 + U(-gain_spread, gain_spread)), delay + U{0..max_dshift}*Ts, numpy default_rng(seed),
+    drawn per plant in the order (gain 2x2, delay shift 2x2).  Returns [draws] 2x2 DTF plants."""
+    from .matlab import c2d_zoh
+
+    K = np.array([[12.8, -18.9], [6.6, -19.4]])
+    tau = np.array([[16.7, 21.0], [10.9, 14.4]])
+    L = np.array([[1.0, 2.0], [2.0, 1.0]])
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(draws):
+        g = 1.0 + rng.uniform(-gain_spread, gain_spread, (2, 2))
+        dl = rng.integers(0, max_dshift + 1, (2, 2))
+        out.append([[c2d_zoh([K[i, j] * g[i, j]], [tau[i, j], 1.0], Ts, L[i, j] + dl[i, j] * Ts)
+                     for j in range(2)] for i in range(2)])
+    return out
+
+
 def dtc_gpc_ww(p=(3, 3), m=(3, 3), lam=(1.0, 1.0), delta=(1.0, 1.0), nit: int = 200, deltak: float = 0.0,
                deltaL: float = 0.0, alfa: float = 0.7, raio: float = 0.8, disturbance: bool = True,
-               filt: bool = True):
+               filt: bool = True, plant=None):
     """DTC_GPC_WW.m:59-164 (config 1), reference structure: every step re-simulates the whole
     history with lsim (plant, disturbance path and the three predictor models), O(nit^2).
-    L = R = I.  Returns dict(y, u, yp, r, q)."""
+    L = R = I.  ``plant``: a 2x2 DTF real plant replacing P of DTC_GPC_WW.m:18-19 (one
+    Monte-Carlo draw of config 4, woodberry_mc_draws); the model stays nominal.
+    Returns dict(y, u, yp, r, q)."""
     P, Pn, Pq = woodberry_models(deltak, deltaL)
+    if plant is not None:
+        P = plant
     my = ny = 2
     Pnz = Pn
     Bp, Ap, dp = descomp_mpc(Pnz)

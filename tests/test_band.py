@@ -308,3 +308,75 @@ def test_band_statuses_in_mixed_batch(gpu):
     for k in (1, 2, 5):
         one = eval_batch(sc, N2[k:k + 1], Nu[k:k + 1], np.zeros((1, 7)), lam[None], r[None], v=v[None])
         np.testing.assert_array_equal(one.J1[0], res.J1[k])
+
+
+def _oracle_vns_terms(ref, oyref, ink=9):
+    """VNS2.m:172-191 from one oracle closed loop: j21 = sum (y - ys)^2, j22 = sum (y - Yref)^2
+    from inK, Jnu = sum (|uopt(:,1)| / |diff(uopt)|)^2 with inf / NaN terms set to 0."""
+    j21 = ((ref.y - ref.ys)[:, ink:] ** 2).sum(1)
+    j22 = ((ref.y - oyref)[:, ink:] ** 2).sum(1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        x = np.abs(ref.uopt[:, :1]) / np.abs(np.diff(ref.uopt, axis=1))
+    x[~np.isfinite(x)] = 0.0
+    return j21, j22, (x ** 2).sum(1)
+
+
+@pytest.mark.gpu
+def test_nonsquare_vns_objective_shell7x5(gpu):
+    """VNS2.m:166-169 on the non-square Shell 7x5 (7 outputs, 3 MVs, 2 measured disturbances):
+    ONE simulation per neighbour with Xsp = every output stepped at inK and Par.mdv, j21 / j22 over
+    the 7 outputs and Jnu over the 3 MVs, F = sum(j21 + j22) + N(1) + sum(Jnu) -- a few
+    neighbours against the oracle's closed loop (oracle/toolbox_band.py)."""
+    from mpct.objectives import vns_objective, vns_refs_nonsquare
+    from mpct.scenarios import SHELL7_TUNED, shell7x5
+    from oracle.scenarios import shell7x5 as o_shell7x5
+    from oracle.toolbox_band import closedloop_band
+
+    sc, r, v, yref = shell7x5(n2_max=40, nu_max=8)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    lam = np.array(SHELL7_TUNED["lam"])
+    cands = [(27, 2, lam), (16, 3, lam * 2.0), (32, 4, np.array([0.2, 0.05, 1.0]))]
+    N2 = np.array([c[0] for c in cands], np.int32)
+    Nu = np.array([c[1] for c in cands], np.int32)
+    L = np.array([c[2] for c in cands])
+    F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, np.zeros((3, 7)), L, mdv=v)
+    assert res.nref == 1 and np.all(res.status == 0), res.status
+    R = vns_refs_nonsquare(7, 200)[0]
+    for k, c in enumerate(cands):
+        ref = closedloop_band(osc, R, ov, c[0], c[1], np.zeros(7), c[2], 200)
+        o21, o22, onu = _oracle_vns_terms(ref, oyref)
+        np.testing.assert_allclose(j21[k], o21, rtol=COST_RTOL, atol=1e-14)
+        np.testing.assert_allclose(j22[k], o22, rtol=COST_RTOL)
+        ok = onu < 1e6
+        np.testing.assert_allclose(jnu[k][ok], onu[ok], rtol=1e-5)
+        Fo = o21.sum() + o22.sum() + c[0] + onu.sum()
+        assert abs(F[k] - Fo) <= 1e-5 * abs(Fo), (k, F[k], Fo)
+
+
+@pytest.mark.gpu
+def test_square_vns_objective_with_mdv_woodberry(gpu):
+    """VNS2.m:148-165 with Par.mdv on a square plant (WoodBerry.m, one measured disturbance): one
+    simulation per output with a unit step on that output only and the disturbance in every
+    simulation; output / MV i from simulation i."""
+    from mpct.objectives import vns_objective
+    from mpct.scenarios import vns_step_refs, woodberry_toolbox
+    from oracle.scenarios import woodberry_toolbox as o_wb
+    from oracle.toolbox_band import closedloop_band
+
+    sc, r, v, yref = woodberry_toolbox()
+    osc, orr, ov, oyref = o_wb()
+    cands = [(12, 3, np.array([1.0, 0.5]), np.array([0.1, 0.2])), (20, 5, np.array([0.3, 1.0]), np.array([0.05, 0.1]))]
+    N2 = np.array([c[0] for c in cands], np.int32)
+    Nu = np.array([c[1] for c in cands], np.int32)
+    F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, np.array([c[2] for c in cands]),
+                                          np.array([c[3] for c in cands]), mdv=v)
+    assert res.nref == 2 and np.all(res.status == 0)
+    refs = vns_step_refs(2, 400)
+    for k, c in enumerate(cands):
+        for i in range(2):
+            ref = closedloop_band(osc, refs[i], ov, c[0], c[1], c[2], c[3], 400)
+            o21, o22, onu = _oracle_vns_terms(ref, oyref)
+            np.testing.assert_allclose(j21[k, i], o21[i], rtol=COST_RTOL)
+            np.testing.assert_allclose(j22[k, i], o22[i], rtol=COST_RTOL)
+            if onu[i] < 1e6:
+                np.testing.assert_allclose(jnu[k, i], onu[i], rtol=1e-5)

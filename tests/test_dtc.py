@@ -83,44 +83,107 @@ def test_dtc_batch_of_candidates(gpu):
     np.testing.assert_allclose(res.J1[0], np.sum((ref["y"] - ref["r"]) ** 2, axis=1), rtol=1e-6)
 
 
-@pytest.mark.gpu
-def test_dtc_monte_carlo_variants(gpu):
-    """Config 4: simulation (c, k) runs plant variant k -- bitwise equal to a single-plant
-    scenario built with that draw, and a uniform-mismatch draw equals the oracle loop."""
-    from mpct.dtc import robust_scores, woodberry_dtc, woodberry_mc
-    from mpct.engine import Scenario, eval_batch
+def test_mc_draws_match_oracle():
+    """Config 4's plant-mismatch draws: the product's (mpct.dtc.woodberry_mc_plants) equal the
+    oracle's restatement of the draw recipe (DTC_GPC_WW.m:18-19) entry by entry."""
+    from mpct.dtc import woodberry_mc_plants
+    from oracle.dtcgpc import woodberry_mc_draws
+
+    mine = woodberry_mc_plants(32)
+    ref = woodberry_mc_draws(32)
+    for Pm, Po in zip(mine, ref):
+        for i in range(2):
+            for j in range(2):
+                a, b = Pm[i][j], Po[i][j]
+                assert a.delay == b.iodelay
+                np.testing.assert_allclose(np.trim_zeros(np.asarray(a.num), "f"), np.trim_zeros(b.num, "f"),
+                                           rtol=1e-13, atol=0)
+                np.testing.assert_allclose(a.den, b.den, rtol=1e-13, atol=0)
+
+
+def test_config4_grid_shape():
+    """SURVEY §8d config 4 grid: p in 3..30, m in 1..min(p, 10), log-uniform weights."""
+    from mpct.dtc import config4_candidates
+
+    N2, Nu, d, l = config4_candidates(10000)
+    assert N2.min() >= 3 and N2.max() <= 30 and Nu.min() >= 1 and np.all(Nu <= np.minimum(N2, 10))
+    assert d.shape == l.shape == (10000, 2) and d.min() >= 1e-3 and l.max() <= 10.0
+    sel = (N2 >= 13) & (Nu >= 7)
+    assert sel.sum() > 100  # the MAXM = 32 range the GPU test below draws from
+
+
+def _oracle_compare(res, C, D, N2, Nu, d, l, pairs, plants):
+    """Compare simulations (c, k) of a plant-variant batch with the reference-structured loop on
+    draw k's plant (oracle.dtcgpc.dtc_gpc_ww(plant=...)): y and u to TRAJ_RTOL of their peak,
+    J1 to 1e-6 relative."""
     from oracle.dtcgpc import dtc_gpc_ww
 
+    worst = 0.0
+    for c, k in pairs:
+        s = c * D + k
+        p, m = int(N2[c]), int(Nu[c])
+        ref = dtc_gpc_ww(p=(p, p), m=(m, m), lam=tuple(l[c]), delta=tuple(d[c]), plant=plants[k])
+        if not np.all(np.isfinite(ref["y"])) or np.max(np.abs(ref["y"])) > 1e6:
+            assert res.status[s] & 4, (c, k, res.status[s])  # the draw destabilises the loop on both sides
+            continue
+        assert res.status[s] == 0, (c, k, res.status[s])
+        ey, eu = _trel(res.y[s], ref["y"]), _trel(res.u[s], ref["u"])
+        J1 = np.sum((ref["y"] - ref["r"]) ** 2, axis=1)
+        ej = float(np.max(np.abs(res.J1[s] - J1) / np.abs(J1)))
+        worst = max(worst, ey, eu)
+        assert ey < TRAJ_RTOL and eu < TRAJ_RTOL, (c, k, p, m, ey, eu)
+        assert ej < 1e-6, (c, k, p, m, ej)
+    return worst
+
+
+@pytest.mark.gpu
+def test_dtc_monte_carlo_variants(gpu):
+    """Config 4 plant variants: simulation (c, k) runs draw k's plant -- each checked against the
+    reference-structured loop on that draw's plant (not against another HIP run)."""
+    from mpct.dtc import robust_scores, woodberry_mc
+    from mpct.engine import eval_batch
+    from oracle.dtcgpc import woodberry_mc_draws
+
     D, C = 4, 6
-    sc, refs, v, plants = woodberry_mc(draws=D, n2_max=10, nu_max=5)
+    sc, refs, v, _ = woodberry_mc(draws=D, n2_max=10, nu_max=5)
+    plants = woodberry_mc_draws(D)
     rng = np.random.default_rng(5)
     N2 = rng.integers(3, 11, C).astype(np.int32)
     Nu = np.minimum(rng.integers(1, 6, C), N2).astype(np.int32)
     d = 10.0 ** rng.uniform(-1, 1, (C, 2))
     l = 10.0 ** rng.uniform(-1, 1, (C, 2))
     res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
-    assert np.all(res.status == 0)
-    for k in (0, 2, 3):
-        one_sc, r, q = woodberry_dtc(n2_max=10, nu_max=5)
-        # the same disturbance paths as the MC scenario, one plant
-        from mpct.dtc import WB_QK, WB_QL, WB_QTAU, mimofilter
-        from mpct.lti import c2d
-        Pq = [[c2d([WB_QK[i]], [WB_QTAU[i], 1.0], 1.0, WB_QL[i])] for i in range(2)]
-        single = Scenario(plants[k], one_sc.model, nu=2, du_min=-np.full(2, np.inf), du_max=np.full(2, np.inf),
-                          u_min=-np.full(2, np.inf), u_max=np.full(2, np.inf), yref=r, n2_max=10, nu_max=5,
-                          window="gpc", weights_squared=False, exact_carima=False, dtc=True,
-                          filters=mimofilter(one_sc.model), dist=Pq)
-        rs = eval_batch(single, N2, Nu, d, l, r[None], v=q[None])
-        np.testing.assert_array_equal(rs.J1, res.J1.reshape(C, D, 2)[:, k])
+    _oracle_compare(res, C, D, N2, Nu, d, l, [(c, k) for c in range(C) for k in (0, 2, 3)], plants)
     mean, worst = robust_scores(res.J1, C, D)
     assert np.all(worst >= mean)
-    # a uniform gain/delay mismatch draw against the reference-structured loop
-    from mpct.dtc import WB_K, WB_L, WB_TAU
-    from mpct.lti import c2d as c2d_
-    Pu = [[c2d_([WB_K[i, j] * 1.1], [WB_TAU[i, j], 1.0], 1.0, WB_L[i, j] + 1.0) for j in range(2)] for i in range(2)]
-    sc2, r2, q2 = woodberry_dtc(n2_max=10, nu_max=5, deltak=0.1, deltaL=1.0)
-    ru = eval_batch(sc2, np.array([3], np.int32), np.array([3], np.int32), np.ones((1, 2)), np.ones((1, 2)),
-                    r2[None], v=q2[None], want_traj=True)
-    ref = dtc_gpc_ww(deltak=0.1, deltaL=1.0)
-    assert _trel(ru.y[0], ref["y"]) < TRAJ_RTOL
-    assert all(Pu[i][j].delay == sc2.plant[i][j].delay for i in range(2) for j in range(2))
+
+
+@pytest.mark.gpu
+def test_config4_range_against_oracle(gpu):
+    """Config 4 at its own workload: candidates of the seeded 10,000-candidate grid with N2 in
+    13..30 and Nu in 7..10 (M = 14..20: the DTC MAXM = 32 kernel instance) on the 32-draw
+    Monte-Carlo scenario of the benchmark, every draw scored in one launch, and a spread of
+    (candidate, draw) pairs compared with DTC_GPC_WW.m's loop on that draw's plant."""
+    from mpct.dtc import config4_candidates, woodberry_mc
+    from mpct.engine import eval_batch
+    from oracle.dtcgpc import woodberry_mc_draws
+
+    D = 32
+    sc, refs, v, _ = woodberry_mc(draws=D, n2_max=30, nu_max=10)
+    N2g, Nug, dg, lg = config4_candidates(10000)
+    idx = np.flatnonzero((N2g >= 13) & (Nug >= 7))[:8]
+    N2, Nu, d, l = N2g[idx], Nug[idx], dg[idx], lg[idx]
+    assert len(np.unique(Nu)) >= 2 and Nu.max() * 2 > 16
+    from mpct.engine import kernel_instance
+
+    assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<32,true,true>"
+    assert kernel_instance(sc) == "gpc_closed_loop_kernel<32,true,false>"
+    res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
+    cost = eval_batch(sc, N2, Nu, d, l, refs, v=v)   # the cost-only instance the bench times
+    ok = res.status == 0
+    np.testing.assert_array_equal(cost.status, res.status)
+    np.testing.assert_allclose(cost.J1[ok], res.J1[ok], rtol=1e-10, atol=0)
+    plants = woodberry_mc_draws(D)
+    pairs = [(c, (5 * c + j * 11) % D) for c in range(len(idx)) for j in range(3)]
+    worst = _oracle_compare(res, len(idx), D, N2, Nu, d, l, pairs, plants)
+    print("config-4 range: %d pairs, max traj rel err %.2e" % (len(pairs), worst))

@@ -228,3 +228,88 @@ def test_two_streams_share_a_scenario(env):
     torch.cuda.synchronize(dev)
     for (out, _), rf in zip(outs, ref):
         assert np.array_equal(out["J1"].cpu().numpy(), rf.J1)
+
+
+@pytest.fixture(scope="module")
+def metric(built, has_gpu):
+    """The benchmark's own scenario: shell3x3(n2_max=30, nu_max=5) -- nu*nu_max = 15, so the
+    cost-only calls launch gpc_closed_loop_kernel<16,false,false> under its VGPR cap (the instance
+    bench.py times), trajectory calls the <16,false,true> instance."""
+    if not has_gpu:
+        pytest.skip("no GPU")
+    from mpct.engine import kernel_instance
+    from mpct.scenarios import shell3x3
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3
+
+    sc, r, yref = shell3x3(n2_max=30, nu_max=5)
+    assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,false,false>"
+    assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<16,false,true>"
+    osc, orr, oyref, _ = o_shell3x3()
+    return dict(sc=sc, r=r, osc=osc, oyref=oyref, cp=CPort(osc, 30, 500, oyref))
+
+
+def test_metric_instance_full_grid(metric):
+    """The exact kernel instance and workload the benchmark times (4096 candidates, N2=30, Nu=5,
+    cost only) against the C port on the whole grid: J1 within COST_RTOL, identical ranking on
+    the Pareto-weighted and the plain sum of costs."""
+    from mpct.engine import eval_batch
+    from mpct.objectives import rank
+    from mpct.scenarios import candidate_grid
+
+    N2, Nu, d, l = candidate_grid(4096)
+    res = eval_batch(metric["sc"], N2, Nu, d, l, metric["r"][None])
+    ref = metric["cp"].eval(N2, Nu, d, l, metric["r"][None], threads=16)
+    assert np.all(res.status == 0) and np.all(ref["status"] == 0)
+    rel = np.max(np.abs(res.J1 - ref["J1"]) / np.abs(ref["J1"]), axis=1)
+    print("metric instance, 4096 grid: J1 max rel %.2e" % rel.max())
+    assert rel.max() < COST_RTOL, (int(np.argmax(rel)), rel.max())
+    w = np.array([0.05, 0.40, 0.55])  # Shell3x3.m:161
+    assert np.array_equal(rank(res.J1 @ w), rank(ref["J1"] @ w))
+    assert np.array_equal(rank(res.J1.sum(1)), rank(ref["J1"].sum(1)))
+
+
+def test_metric_instance_numpy_oracle_sample(metric):
+    """16 candidates of the metric grid through the timed instance against the independent numpy
+    oracle (primal active-set QP on the least-squares form, oracle/toolbox_gpc.py): J1 within
+    COST_RTOL and the same ranking."""
+    from mpct.engine import eval_batch
+    from mpct.objectives import rank
+    from mpct.scenarios import candidate_grid
+    from oracle.toolbox_gpc import closedloop_toolbox as o_cl
+
+    N2, Nu, d, l = candidate_grid(4096)
+    pick = np.r_[0, np.random.default_rng(7).choice(np.arange(1, 4096), 15, replace=False)]
+    res = eval_batch(metric["sc"], N2[pick], Nu[pick], d[pick], l[pick], metric["r"][None])
+    J = np.zeros((16, 3))
+    for k, c in enumerate(pick):
+        o = o_cl(metric["osc"], metric["r"], None, 30, 5, d[c], l[c], 500, open_loop=False)
+        J[k] = ((o.y - metric["oyref"]) ** 2).sum(axis=1)
+    rel = np.max(np.abs(res.J1 - J) / np.abs(J))
+    print("metric instance vs numpy oracle: J1 max rel %.2e" % rel)
+    assert rel < COST_RTOL
+    w = np.array([0.05, 0.40, 0.55])
+    assert np.array_equal(rank(res.J1 @ w), rank(J @ w))
+
+
+def test_multi_device_entry_equals_single(metric):
+    """mpct_eval_batch_multi on the devices this box has: bitwise equal to mpct_eval_batch
+    (ndev = 1 here; with more GPUs every shard runs the same kernel on its own device)."""
+    import torch
+
+    from mpct.engine import eval_batch, eval_batch_multi
+    from mpct.scenarios import candidate_grid
+
+    N2, Nu, d, l = candidate_grid(1000)
+    devs = list(range(torch.cuda.device_count()))
+    a = eval_batch(metric["sc"], N2, Nu, d, l, metric["r"][None], device=0)
+    b = eval_batch_multi(metric["sc"], devs, N2, Nu, d, l, metric["r"][None])
+    assert np.array_equal(a.J1, b.J1) and np.array_equal(a.status, b.status)
+    assert np.array_equal(a.qp_iters, b.qp_iters)
+    # open-loop + trajectories through the same entry (every result array is sharded)
+    c = eval_batch(metric["sc"], N2[:8], Nu[:8], d[:8], l[:8], metric["r"][None], open_loop=True,
+                   want_traj=True, device=0)
+    e = eval_batch_multi(metric["sc"], devs, N2[:8], Nu[:8], d[:8], l[:8], metric["r"][None], open_loop=True,
+                         want_traj=True)
+    for k in ("J1", "j21", "j22", "Jnu", "y", "u", "ys", "uopt"):
+        assert np.array_equal(getattr(c, k), getattr(e, k)), k

@@ -120,13 +120,29 @@ def test_tuning_parameters_roundtrip(tmp_path):
     from scipy.io import loadmat
 
     p = str(tmp_path / "Shell3x3_Tuning_test.mat")
+    import datetime
+
+    from mpct.tuning import scale_record
+
     save_tuning_parameters(p, [24, 24, 24], [6, 2, 2], [0.01, 0.004, 0.0008], [9e-5, 5e-4, 1.5e-3],
-                           scale={"L": np.eye(3), "R": np.eye(3)}, date="15-Oct-2026 12:00:00")
-    m = loadmat(p, squeeze_me=True, struct_as_record=False)["Tuning_Parameters"]
-    assert int(m.N) == 24
-    np.testing.assert_array_equal(np.atleast_1d(m.Nu), [6, 2, 2])
-    np.testing.assert_allclose(np.atleast_1d(m.delta), [0.01, 0.004, 0.0008])
-    np.testing.assert_allclose(m.scale.L, np.eye(3))
+                           scale={"L": np.eye(3), "R": np.diag([0.5, 0.25, 0.125])},
+                           date=datetime.datetime(2026, 10, 15, 12, 0, 0))
+    m = loadmat(p, squeeze_me=False, struct_as_record=False)["Tuning_Parameters"][0, 0]
+    assert int(m.N[0, 0]) == 24
+    np.testing.assert_array_equal(m.Nu, [[6, 2, 2]])
+    np.testing.assert_allclose(m.delta, [[0.01, 0.004, 0.0008]])
+    sc = m.scale[0, 0]
+    np.testing.assert_allclose(sc.L, np.eye(3))
+    # MPCTuning.m:156-160: Ru = R(1:ny,1:ny), Rv = R(ny+1:end,...) (0x0 without MDs); the
+    # resume path of Shell3x3.m:180-183 reads all four fields
+    np.testing.assert_allclose(sc.Ru, np.diag([0.5, 0.25, 0.125]))
+    assert sc.Rv.size == 0
+    # datetime cannot be written outside MATLAB: its datenum (datenum(2026,10,15,12,0,0))
+    assert float(m.date[0, 0]) == 740270.5
+    # Shell 7x5: R is 5x5 over 3 MVs and 2 MDs -> Rv is the 2x2 MD block
+    r5 = scale_record(np.ones(7), np.arange(1.0, 6.0), 3)
+    np.testing.assert_allclose(r5["Rv"], np.diag([4.0, 5.0]))
+    assert r5["Ru"].shape == (3, 3)
     j = str(tmp_path / "t.json")
     rec = save_tuning_parameters(j, [12], [4, 2, 2], [1, 1, 1], [1, 1, 1])
     assert rec["N"] == 12
@@ -169,3 +185,101 @@ def test_vns2_batched_equals_sequential_cport(built):
     np.testing.assert_array_equal(seq[1], bat[1])
     assert seq[4] == bat[4] and seq[6] == bat[6]
     assert seq[4] < 1e30
+
+
+def _stub_eval(statuses):
+    """A stand-in for mpct.engine.eval_batch (no GPU): smooth finite costs of the weights, and the
+    statuses given (cycled over the simulations)."""
+    from mpct.engine import EvalResult
+
+    def ev(sc, N2, Nu, delta, lam, refs, v=None, open_loop=False, want_traj=False, device=-1, **kw):
+        N2 = np.atleast_1d(N2)
+        C_ = N2.size
+        refs = np.asarray(refs).reshape(-1, sc.my, sc.nit)
+        S = C_ * refs.shape[0]
+        d = np.repeat(np.asarray(delta, float).reshape(C_, sc.my), refs.shape[0], axis=0)
+        l_ = np.repeat(np.asarray(lam, float).reshape(C_, sc.nu), refs.shape[0], axis=0)
+        J1 = (np.log10(d + 1e-9) + 1.0) ** 2 + l_.sum(1, keepdims=True) + 1.0
+        st = np.resize(np.asarray(statuses, dtype=np.int32), S)
+        ev.calls.append(dict(nref=refs.shape[0], v=v, open_loop=open_loop))
+        return EvalResult(J1=J1, j21=J1 * 0.5, j22=J1 * 0.25, Jnu=np.ones((S, sc.nu)), status=st,
+                          qp_iters=np.zeros(S, np.int64), nref=refs.shape[0])
+
+    ev.calls = []
+    return ev
+
+
+class _Sc:
+    def __init__(self, my, nu, nit=50):
+        self.my, self.nu, self.nit, self.nd, self.nq = my, nu, nit, 0, 0
+
+
+def test_iteration_caps_keep_finite_costs(monkeypatch):
+    """only the fatal status bits (QP infeasible, non-finite, skipped, bad horizon)
+    score NaN; QP_MAXITER (1), SQP_MAXITER (32) and BOUNDS (64) keep the last iterate's finite
+    cost as mpcmove / nlmpcmove do (closedloop_toolbox_nmpc.m:69), so GAM's finite differences
+    and goal-attainment constraints stay finite."""
+    import mpct.engine
+    import mpct.objectives
+    from mpct.objectives import failed
+    from mpct.tuning import engine_evaluators
+
+    assert list(failed([0, 1, 2, 4, 8, 16, 32, 64, 33, 34])) == [False, False, True, True, True, True, False,
+                                                                  False, False, True]
+    stub = _stub_eval([32, 1, 64, 0])
+    monkeypatch.setattr(mpct.engine, "eval_batch", stub)
+    monkeypatch.setattr(mpct.objectives, "eval_batch", stub)
+    par = TuningPar(my=2, ny=2, nbp=5, nbc=4, w=np.array([0.1, 0.5]), q0=np.ones(2), w0=np.full(2, 0.1))
+    bj1, bvns = engine_evaluators(_Sc(2, 2), np.zeros((2, 50)), par)
+    J = bj1(np.array([[1.0, 1.0, 0.1, 0.1], [0.5, 2.0, 0.2, 0.1]]))
+    assert np.all(np.isfinite(J))
+    x, attain, Fx, nb = gam_fgoalattain(par, bj1, max_iter=5)
+    assert np.all(np.isfinite(x)) and np.isfinite(attain) and np.all(np.isfinite(Fx))
+    assert np.all(np.isfinite(bvns([((31, 31), (2, 2)), ((15, 15), (3, 3))], [1, 1], [0.1, 0.1])))
+    # a fatal bit on any of a candidate's simulations makes its VNS score NaN (never improves)
+    stub2 = _stub_eval([0, 2])
+    monkeypatch.setattr(mpct.objectives, "eval_batch", stub2)
+    monkeypatch.setattr(mpct.engine, "eval_batch", stub2)
+    bj1, bvns = engine_evaluators(_Sc(2, 2), np.zeros((2, 50)), par)
+    F = bvns([((31, 31), (2, 2))], [1, 1], [0.1, 0.1])
+    assert np.isnan(F[0])
+    J = bj1(np.array([[1.0, 1.0, 0.1, 0.1], [0.5, 2.0, 0.2, 0.1]]))
+    assert np.isfinite(J[0]).all() and np.isnan(J[1]).all()
+
+
+def test_nonsquare_vns_and_mdv(monkeypatch):
+    """VNS2.m:166-169: a non-square plant is simulated ONCE per neighbour with Xsp (every output
+    stepped at inK, VNS2.m:58-61), j21/j22 over its my outputs and Jnu over its nu MVs, F =
+    sum(j21 + j22) + N(1) + sum(Jnu); Par.mdv reaches every simulation (VNS2.m:153,168,
+    GAM_fun.m:81)."""
+    import mpct.engine
+    import mpct.objectives
+    from mpct.objectives import vns_objective
+    from mpct.tuning import engine_evaluators
+
+    stub = _stub_eval([0])
+    monkeypatch.setattr(mpct.objectives, "eval_batch", stub)
+    monkeypatch.setattr(mpct.engine, "eval_batch", stub)
+    sc = _Sc(7, 3, nit=40)
+    mdv = np.ones((2, 40))
+    d = np.full((2, 7), 0.0)
+    l_ = np.full((2, 3), 0.1)
+    F, j21, j22, jnu, res = vns_objective(sc, [27, 16], [2, 3], d, l_, mdv=mdv)
+    c = stub.calls[-1]
+    assert c["nref"] == 1 and c["open_loop"] and c["v"].shape == (1, 2, 40)
+    assert j21.shape == (2, 7) and jnu.shape == (2, 3)
+    np.testing.assert_allclose(F, j21.sum(1) + j22.sum(1) + np.array([27, 16]) + jnu.sum(1))
+    from mpct.objectives import vns_refs_nonsquare
+
+    R = vns_refs_nonsquare(7, 40)
+    assert R.shape == (1, 7, 40) and np.all(R[0, :, 9:] == 1) and np.all(R[0, :, :9] == 0)
+    # square plants: one simulation per output, MDs to each
+    sq = _Sc(2, 2, nit=40)
+    vns_objective(sq, [10], [2], np.ones((1, 2)), np.ones((1, 2)), mdv=np.ones((1, 40)))
+    assert stub.calls[-1]["nref"] == 2 and stub.calls[-1]["v"].shape == (1, 1, 40)
+    par = TuningPar(my=7, ny=3, nbp=7, nbc=4, w=np.ones(7), q0=np.zeros(7), w0=np.full(3, 0.1))
+    bj1, bvns = engine_evaluators(sc, np.zeros((7, 40)), par, mdv=mdv)
+    bj1(np.ones((1, 10)))
+    assert stub.calls[-1]["v"].shape == (1, 2, 40) and not stub.calls[-1]["open_loop"]
+    bvns([((27,) * 7, (2, 2, 2))], np.zeros(7), [0.1] * 3)
+    assert stub.calls[-1]["nref"] == 1 and stub.calls[-1]["v"] is not None

@@ -3,33 +3,15 @@ MPCTuning(nlobj_proj, r, lineal=false, w=[0.7 0.3], nit, Yref, mdv, nbp=5, nbc=4
 the GPU engine: GAM weights + VNS horizons alternated as MPC_TFob.m, Tuning_Parameters written
 like MPCTuning.m:374-381.  Initial weights: the nlmpc object's delta = [1 1], lambda = [0.1 0.1]
 (VanDeVusse_NMPC.m:193-198).  python tools/tune_vandevusse.py [out.mat] [gam_max_iter]"""
-import os
 import sys
-import threading
-import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "model-predictive-control-tuning_amd"), ROOT]
-from mpct.nmpc import VDV_W, vandevusse  # noqa: E402
-from mpct.tuning import mpc_tuning  # noqa: E402
+from tune_common import run
+from mpct.nmpc import VDV_W, vandevusse
 
-out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "VanDeVusse_NMPC_Tuning.mat")
+out = sys.argv[1] if len(sys.argv) > 1 else None
 gmax = int(sys.argv[2]) if len(sys.argv) > 2 else 400
 sc, r, yref = vandevusse(n_max=31, nu_max=15)
-t0 = time.time()
-
-
-def _heartbeat():
-    # a GAM phase can run minutes without a log line: say so every minute
-    while True:
-        time.sleep(60)
-        print("... tuning, %.0f s" % (time.time() - t0), flush=True)
-
-
-threading.Thread(target=_heartbeat, daemon=True).start()
-N, Nu, delta, lam, Fob = mpc_tuning(sc, r, my=2, ny=2, w=VDV_W, nbp=5, nbc=4, dmin=np.zeros(2, dtype=int),
-                                    q0=np.array([1.0, 1.0]), w0=np.array([0.1, 0.1]), log=lambda *a: print(*a, flush=True), save_path=out,
-                                    gam_max_iter=gmax, lineal=False)
-print("N=%s Nu=%s delta=%s lambda=%s Fob=%s  (%.1f s)" % (N, Nu, delta, lam, Fob, time.time() - t0))
+run("VanDeVusse_NMPC", sc, r, 2, 2, VDV_W, 5, 4, np.zeros(2, dtype=int), q0=np.array([1.0, 1.0]),
+    w0=np.array([0.1, 0.1]), lineal=False, out=out, gam_max_iter=gmax)
