@@ -72,7 +72,10 @@ typedef struct mpct_dtf {
  *   carima_A / carima_B : the CARIMA form after descompMPC + BA_MIMO (DTC_GPC_WW.m:79):
  *                         A_i (na[i]+1 coeffs, z^-1 powers, A_i[0]=1) concatenated over i;
  *                         B_ij (nb[i*(nu+nd)+j]+1 coeffs) concatenated row-major over (i,j);
- *                         dp[i*(nu+nd)+j] the descompMPC delays.
+ *                         dp[i*(nu+nd)+j] the descompMPC delays.  abi >= 5, dtc == 0, mdband == 0:
+ *                         na, carima_A, nb, carima_B and dp may ALL be NULL; the library then
+ *                         derives them from `model` (descompMPC.m:19-43, then the exact LCM of
+ *                         each row's distinct denominators: the toolbox-equivalent CARIMA form).
  *   n1[i]               : first predicted step of output i: 1 = toolbox window t+1..t+N2
  *                         (PredictionHorizon semantics), dmin_i+1 = GPC window (MatG.m:64,
  *                         diophantine.m:44 N1 = d+1)

@@ -1,0 +1,452 @@
+/* mpct_mex.c — MATLAB MEX gateway of libmpct (include/mpct.h): the drop-in boundary the MATLAB
+ * host of the reference calls in place of its per-candidate closed loop
+ *   [y,u,t,ys,uopt] = closedloop_toolbox(mpc_toolbox,r,v,N,Nu,delta,lambda,nit)
+ *   (MPC-Tuning/MPC_Tuning/closedloop_toolbox.m:1; callers VNS2.m:153,168, GAM_fun.m:81) and its
+ *   NMPC twin closedloop_toolbox_nmpc.m:1 (VNS2.m:155, GAM_fun.m:87).
+ * The .m wrappers next to this file (closedloop_toolbox.m, closedloop_gpc_batch.m,
+ * closedloop_toolbox_nmpc.m, mpct_scenario_from_mpc.m) build the descriptor structs from the
+ * reference's own mpc / nlmpc objects and call:
+ *
+ *   v = mpct_mex('version')                          ABI version of the loaded libmpct
+ *   h = mpct_mex('create', desc)                     linear scenario (mpct_scenario_create)
+ *   h = mpct_mex('create_nmpc', desc)                NMPC scenario (mpct_nmpc_scenario_create)
+ *   [J1,j21,j22,Jnu,status,iters,y,u,ys,uopt] = mpct_mex('eval', h, N2, Nu, delta, lambda, r, v, opts)
+ *   [...] = mpct_mex('eval_multi', h, devices, N2, Nu, delta, lambda, r, v, opts)
+ *   name = mpct_mex('instance', h, opts)             kernel instance an eval launches
+ *   mpct_mex('destroy', h)
+ *
+ * MATLAB layouts (column-major, what the callers already hold):
+ *   N2, Nu       C-vectors (any numeric class; converted to int32)
+ *   delta        C x my,  lambda  C x nu  (one candidate per row)
+ *   r            my x nit (one reference set, Xsp) or my x nit x nref (VNS: one per output)
+ *   v            nv x nit or nv x nit x nref, nv = nd + nq ([] when there are none)
+ *   opts         struct, optional fields open_loop, want_traj, max_qp_iter, device, feas_tol
+ * Outputs, simulation s = (c-1)*nref + k:  J1/j21/j22  S x my,  Jnu  S x nu,  status/iters  S x 1,
+ *   y/ys  my x nit x S,  u/uopt  nu x nit x S  (row signals, as closedloop_toolbox returns them).
+ * Descriptor structs: the fields of mpct_scenario_desc / mpct_nmpc_desc by name; plant, model,
+ *   filter, dist are struct arrays (my x ncols) with fields num, den (row vectors, tfdata 'v'
+ *   form) and delay; plant_var is an nplant x (my*ncols) struct array; yref is my x nit.
+ *
+ * Ownership and errors: prhs are read-only; every output is created here and handed
+ * to MATLAB.  Arguments are validated before anything is allocated (mexErrMsgIdAndTxt unwinds);
+ * library errors become mexErrMsgIdAndTxt("mpct:<call>", mpct_last_error()).  Per-candidate
+ * numerical trouble is never an error: it is status(s) with NaN costs, like the reference's
+ * try/catch + fprintf (VNS2.m:161-163).  Scenario handles are uint64 keys into a registry, so a
+ * stale or foreign handle is an error, not a crash; mexAtExit destroys every live scenario.
+ * MATLAB calls mexFunction on one thread; all GPU work of a call is joined before it returns.
+ *
+ * Build (MATLAB, Linux, ROCm):  mex -R2018a matlab/mpct_mex.c -Iinclude ...
+ *   -Lmodel-predictive-control-tuning_amd/csrc -lmpct LDFLAGS='$LDFLAGS -Wl,-rpath,<csrc>'
+ *   (matlab/build_mpct_mex.m).  In this repository it is compiled against tests/mex_stub/mex.h. */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mex.h"
+#include "mpct.h"
+
+#define MPCT_MEX_MAX 256
+static mpct_scenario* g_live[MPCT_MEX_MAX];
+static int g_atexit = 0;
+
+static void destroy_all(void) {
+  for (int k = 0; k < MPCT_MEX_MAX; ++k)
+    if (g_live[k]) {
+      mpct_scenario_destroy(g_live[k]);
+      g_live[k] = NULL;
+    }
+}
+
+static void lib_error(const char* id) { mexErrMsgIdAndTxt(id, "%s", mpct_last_error()); }
+
+/* ---------------------------------------------------------------------------------------------
+ * small argument readers (validate first, allocate afterwards) */
+static const mxArray* field(const mxArray* s, const char* name, int required) {
+  const mxArray* f = mxGetField(s, 0, name);
+  if (!f && required) mexErrMsgIdAndTxt("mpct:desc", "descriptor field '%s' is missing", name);
+  return (f && mxIsEmpty(f) && !required) ? NULL : f;
+}
+
+static double scalar(const mxArray* a, const char* what) {
+  if (!a || !mxIsNumeric(a) || mxGetNumberOfElements(a) != 1)
+    mexErrMsgIdAndTxt("mpct:arg", "'%s' must be a numeric scalar", what);
+  return mxGetScalar(a);
+}
+
+static double fscalar(const mxArray* s, const char* name, double dflt) {
+  const mxArray* f = mxGetField(s, 0, name);
+  return (f && !mxIsEmpty(f)) ? scalar(f, name) : dflt;
+}
+
+/* a numeric array as doubles (copied, caller frees), n elements checked when n >= 0 */
+static double* doubles(const mxArray* a, long n, const char* what) {
+  if (!a || !mxIsNumeric(a) || mxIsComplex(a) || mxIsSparse(a))
+    mexErrMsgIdAndTxt("mpct:arg", "'%s' must be a real full numeric array", what);
+  const size_t m = mxGetNumberOfElements(a);
+  if (n >= 0 && (long)m != n) mexErrMsgIdAndTxt("mpct:arg", "'%s' must have %ld elements (has %zu)", what, n, m);
+  double* out = (double*)mxMalloc((m ? m : 1) * sizeof(double));
+  if (mxIsDouble(a)) {
+    memcpy(out, mxGetPr(a), m * sizeof(double));
+  } else {
+    const mxClassID c = mxGetClassID(a);
+    const void* p = mxGetData(a);
+    for (size_t k = 0; k < m; ++k) {
+      switch (c) {
+        case mxINT32_CLASS: out[k] = ((const int32_t*)p)[k]; break;
+        case mxINT64_CLASS: out[k] = (double)((const int64_t*)p)[k]; break;
+        case mxUINT64_CLASS: out[k] = (double)((const uint64_t*)p)[k]; break;
+        case mxSINGLE_CLASS: out[k] = ((const float*)p)[k]; break;
+        case mxUINT8_CLASS: out[k] = ((const uint8_t*)p)[k]; break;
+        default: mexErrMsgIdAndTxt("mpct:arg", "'%s': unsupported numeric class", what);
+      }
+    }
+  }
+  return out;
+}
+
+static int32_t* ints(const mxArray* a, long n, const char* what) {
+  double* d = doubles(a, n, what);
+  const size_t m = mxGetNumberOfElements(a);
+  int32_t* out = (int32_t*)mxMalloc((m ? m : 1) * sizeof(int32_t));
+  for (size_t k = 0; k < m; ++k) {
+    if (d[k] != floor(d[k]) || fabs(d[k]) > 2147483647.0) mexErrMsgIdAndTxt("mpct:arg", "'%s' must hold integers", what);
+    out[k] = (int32_t)d[k];
+  }
+  mxFree(d);
+  return out;
+}
+
+/* struct array of transfer functions (fields num, den, delay) -> mpct_dtf[n] (row-major order
+ * i*ncols + j of an my x ncols MATLAB struct matrix; MATLAB stores it column-major) */
+static mpct_dtf* dtfs(const mxArray* a, int rows, int cols, const char* what) {
+  if (!a || !mxIsStruct(a) || (int)mxGetNumberOfElements(a) != rows * cols)
+    mexErrMsgIdAndTxt("mpct:desc", "'%s' must be a %d x %d struct array (num, den, delay)", what, rows, cols);
+  mpct_dtf* out = (mpct_dtf*)mxCalloc((size_t)rows * cols, sizeof(mpct_dtf));
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) {
+      const size_t idx = (size_t)j * rows + i; /* column-major element (i, j) */
+      const mxArray* num = mxGetField(a, idx, "num");
+      const mxArray* den = mxGetField(a, idx, "den");
+      const mxArray* dl = mxGetField(a, idx, "delay");
+      if (!num || !den || !dl) mexErrMsgIdAndTxt("mpct:desc", "'%s' needs fields num, den, delay", what);
+      const long n = (long)mxGetNumberOfElements(den);
+      if (n < 1 || (long)mxGetNumberOfElements(num) > n)
+        mexErrMsgIdAndTxt("mpct:desc", "'%s'(%d,%d): den empty or num longer than den", what, i + 1, j + 1);
+      double* nn = (double*)mxCalloc((size_t)n, sizeof(double));
+      double* src = doubles(num, -1, what);
+      const long m = (long)mxGetNumberOfElements(num);
+      memcpy(nn + (n - m), src, (size_t)m * sizeof(double)); /* tfdata 'v': numerator padded in front */
+      mxFree(src);
+      mpct_dtf* e = &out[(size_t)i * cols + j];
+      e->len = (int32_t)n;
+      e->num = nn;
+      e->den = doubles(den, n, what);
+      e->delay = (int32_t)scalar(dl, "delay");
+    }
+  return out;
+}
+
+/* row signals: MATLAB rows x nit [x nref] (column-major) -> C [nref][rows][nit] (row-major) */
+static double* signals(const mxArray* a, int rows, int nit, int* nref, const char* what) {
+  if (!a || !mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("mpct:arg", "'%s' must be a real double array", what);
+  const mwSize nd = mxGetNumberOfDimensions(a);
+  const mwSize* dims = mxGetDimensions(a);
+  const int k = nd >= 3 ? (int)dims[2] : 1;
+  if (nd > 3 || (int)dims[0] != rows || (int)dims[1] != nit)
+    mexErrMsgIdAndTxt("mpct:arg", "'%s' must be %d x %d (x nref)", what, rows, nit);
+  if (*nref > 0 && k != *nref && k != 1) mexErrMsgIdAndTxt("mpct:arg", "'%s' must have 1 or %d pages", what, *nref);
+  const int pages = *nref > 0 ? *nref : k;
+  const double* p = mxGetPr(a);
+  const size_t total = (size_t)pages * (size_t)rows * (size_t)nit;
+  double* out = (double*)mxMalloc((total > 0 ? total : 1) * sizeof(double));
+  for (int q = 0; q < pages; ++q)
+    for (int i = 0; i < rows; ++i)
+      for (int t = 0; t < nit; ++t) out[((size_t)q * rows + i) * nit + t] = p[(size_t)(k == 1 ? 0 : q) * rows * nit + (size_t)t * rows + i];
+  *nref = pages;
+  return out;
+}
+
+/* C x w MATLAB matrix -> row-major [C][w] */
+static double* rows_of(const mxArray* a, long C, int w, const char* what) {
+  if (!a || !mxIsNumeric(a) || (long)mxGetM(a) != C || (int)mxGetN(a) != w)
+    mexErrMsgIdAndTxt("mpct:arg", "'%s' must be %ld x %d (one candidate per row)", what, C, w);
+  double* d = doubles(a, C * w, what);
+  double* out = (double*)mxMalloc(((C > 0 && w > 0) ? (size_t)C * w : 1) * sizeof(double));
+  for (long c = 0; c < C; ++c)
+    for (int i = 0; i < w; ++i) out[c * w + i] = d[(size_t)i * C + c];
+  mxFree(d);
+  return out;
+}
+
+static mpct_scenario* handle(const mxArray* a) {
+  if (!a || mxGetClassID(a) != mxUINT64_CLASS || mxGetNumberOfElements(a) != 1)
+    mexErrMsgIdAndTxt("mpct:handle", "scenario handle must be a uint64 scalar from mpct_mex('create', ...)");
+  const uint64_t h = *(const uint64_t*)mxGetData(a);
+  if (h < 1 || h > MPCT_MEX_MAX || !g_live[h - 1]) mexErrMsgIdAndTxt("mpct:handle", "stale or unknown scenario handle");
+  return g_live[h - 1];
+}
+
+static mxArray* new_handle(mpct_scenario* s) {
+  for (int k = 0; k < MPCT_MEX_MAX; ++k)
+    if (!g_live[k]) {
+      g_live[k] = s;
+      mxArray* h = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
+      *(uint64_t*)mxGetData(h) = (uint64_t)(k + 1);
+      return h;
+    }
+  mpct_scenario_destroy(s);
+  mexErrMsgIdAndTxt("mpct:handle", "too many live scenarios (%d)", MPCT_MEX_MAX);
+  return NULL;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * commands */
+static int32_t idim(const mxArray* s, const char* name) { return (int32_t)scalar(field(s, name, 1), name); }
+
+static void cmd_create(int nlhs, mxArray* plhs[], const mxArray* d) {
+  if (!mxIsStruct(d)) mexErrMsgIdAndTxt("mpct:desc", "descriptor must be a struct");
+  mpct_scenario_desc D;
+  memset(&D, 0, sizeof D);
+  D.abi_version = MPCT_ABI_VERSION;
+  D.my = idim(d, "my");
+  D.nu = idim(d, "nu");
+  D.nd = (int32_t)fscalar(d, "nd", 0);
+  D.nit = idim(d, "nit");
+  D.n2_max = idim(d, "n2_max");
+  D.nu_max = idim(d, "nu_max");
+  D.weights_squared = (int32_t)fscalar(d, "weights_squared", 1);
+  D.vns_ink = (int32_t)fscalar(d, "vns_ink", 10);
+  if (D.my < 1 || D.nu < 1 || D.nd < 0 || D.nit < 1) mexErrMsgIdAndTxt("mpct:desc", "non-positive dimension");
+  const int nin = D.nu + D.nd, my = D.my;
+  const mxArray* n1 = field(d, "n1", 0);
+  if (n1) {
+    D.n1 = ints(n1, my, "n1");
+  } else { /* the toolbox window t+1..t+N2 (PredictionHorizon semantics) */
+    int32_t* w = (int32_t*)mxMalloc((size_t)my * sizeof(int32_t));
+    for (int i = 0; i < my; ++i) w[i] = 1;
+    D.n1 = w;
+  }
+  D.plant = dtfs(field(d, "plant", 1), my, nin, "plant");
+  D.model = field(d, "model", 0) ? dtfs(field(d, "model", 0), my, nin, "model") : D.plant;
+  if (field(d, "na", 0)) { /* explicit CARIMA tables (DTC / rounded LCM); else derived by the library */
+    D.na = ints(field(d, "na", 1), my, "na");
+    D.nb = ints(field(d, "nb", 1), (long)my * nin, "nb");
+    D.dp = ints(field(d, "dp", 1), (long)my * nin, "dp");
+    D.carima_A = doubles(field(d, "carima_A", 1), -1, "carima_A");
+    D.carima_B = doubles(field(d, "carima_B", 1), -1, "carima_B");
+  }
+  D.du_min = doubles(field(d, "du_min", 1), D.nu, "du_min");
+  D.du_max = doubles(field(d, "du_max", 1), D.nu, "du_max");
+  D.u_min = doubles(field(d, "u_min", 1), D.nu, "u_min");
+  D.u_max = doubles(field(d, "u_max", 1), D.nu, "u_max");
+  int one = 1;
+  D.yref = signals(field(d, "yref", 1), my, D.nit, &one, "yref");
+  D.dtc = (int32_t)fscalar(d, "dtc", 0);
+  if (field(d, "filter", 0)) D.filter = dtfs(field(d, "filter", 0), my, 1, "filter");
+  D.nq = (int32_t)fscalar(d, "nq", 0);
+  if (D.nq > 0) D.dist = dtfs(field(d, "dist", 1), my, D.nq, "dist");
+  D.nplant = (int32_t)fscalar(d, "nplant", 0);
+  if (D.nplant > 1) D.plant_var = dtfs(field(d, "plant_var", 1), D.nplant * my, nin, "plant_var");
+  D.mdband = (int32_t)fscalar(d, "mdband", D.nd > 0 ? 1 : 0);
+  if (D.mdband) {
+    D.y_min = doubles(field(d, "y_min", 1), my, "y_min");
+    D.y_max = doubles(field(d, "y_max", 1), my, "y_max");
+    D.ecr_min = doubles(field(d, "ecr_min", 1), my, "ecr_min");
+    D.ecr_max = doubles(field(d, "ecr_max", 1), my, "ecr_max");
+    if (field(d, "y_scale", 0)) D.y_scale = doubles(field(d, "y_scale", 0), my, "y_scale");
+    if (field(d, "u_scale", 0)) D.u_scale = doubles(field(d, "u_scale", 0), D.nu, "u_scale");
+    D.rho_ecr = fscalar(d, "rho_ecr", 1e4);
+  }
+  mpct_scenario* s = NULL;
+  if (mpct_scenario_create(&D, &s) != MPCT_OK) lib_error("mpct:create");
+  if (nlhs >= 0) plhs[0] = new_handle(s);
+}
+
+static void cmd_create_nmpc(mxArray* plhs[], const mxArray* d) {
+  if (!mxIsStruct(d)) mexErrMsgIdAndTxt("mpct:desc", "descriptor must be a struct");
+  mpct_nmpc_desc D;
+  memset(&D, 0, sizeof D);
+  D.abi_version = MPCT_ABI_VERSION;
+  D.model = (int32_t)fscalar(d, "model", MPCT_NMPC_VANDEVUSSE);
+  D.nx = idim(d, "nx");
+  D.ny = idim(d, "ny");
+  D.nu = idim(d, "nu");
+  if (D.nx < 1 || D.ny < 1 || D.nu < 1) mexErrMsgIdAndTxt("mpct:desc", "non-positive dimension");
+  if (field(d, "params", 0)) D.params = doubles(field(d, "params", 0), 16, "params");
+  D.xc = ints(field(d, "xc", 1), D.ny, "xc");
+  D.ts = scalar(field(d, "ts", 1), "ts");
+  D.nsub = (int32_t)fscalar(d, "nsub", 10);
+  D.x0 = doubles(field(d, "x0", 1), D.nx, "x0");
+  D.u0 = doubles(field(d, "u0", 1), D.nu, "u0");
+  D.u_min = doubles(field(d, "u_min", 1), D.nu, "u_min");
+  D.u_max = doubles(field(d, "u_max", 1), D.nu, "u_max");
+  if (field(d, "x_min", 0)) D.x_min = doubles(field(d, "x_min", 0), D.nx, "x_min");
+  if (field(d, "x_max", 0)) D.x_max = doubles(field(d, "x_max", 0), D.nx, "x_max");
+  if (field(d, "y_scale", 0)) D.y_scale = doubles(field(d, "y_scale", 0), D.ny, "y_scale");
+  if (field(d, "u_scale", 0)) D.u_scale = doubles(field(d, "u_scale", 0), D.nu, "u_scale");
+  D.n_max = idim(d, "n_max");
+  D.nu_max = idim(d, "nu_max");
+  D.nit = idim(d, "nit");
+  int one = 1;
+  D.yref = signals(field(d, "yref", 1), D.ny, D.nit, &one, "yref");
+  D.vns_ink = (int32_t)fscalar(d, "vns_ink", 10);
+  D.sqp_max = (int32_t)fscalar(d, "sqp_max", 0);
+  D.sqp_tol = fscalar(d, "sqp_tol", 0.0);
+  mpct_scenario* s = NULL;
+  if (mpct_nmpc_scenario_create(&D, &s) != MPCT_OK) lib_error("mpct:create_nmpc");
+  plhs[0] = new_handle(s);
+}
+
+/* the scenario's dimensions from the library (mpct_scenario_table which = 2) */
+static void dims_of(mpct_scenario* s, int* my, int* nu, int* nd) {
+  double dm[9];
+  if (mpct_scenario_table(s, 2, dm, 9) < 9) lib_error("mpct:eval");
+  *my = (int)dm[0];
+  *nu = (int)dm[1];
+  *nd = (int)dm[2];
+}
+
+static mpct_opts read_opts(const mxArray* o) {
+  mpct_opts r = {0, 0, 0, -1, 0.0};
+  if (!o || mxIsEmpty(o)) return r;
+  if (!mxIsStruct(o)) mexErrMsgIdAndTxt("mpct:arg", "opts must be a struct");
+  r.open_loop = (int32_t)fscalar(o, "open_loop", 0);
+  r.want_traj = (int32_t)fscalar(o, "want_traj", 0);
+  r.max_qp_iter = (int32_t)fscalar(o, "max_qp_iter", 0);
+  r.device = (int32_t)fscalar(o, "device", -1);
+  r.feas_tol = fscalar(o, "feas_tol", 0.0);
+  return r;
+}
+
+/* C row-major [S][w] -> MATLAB S x w */
+static mxArray* out_rows(const double* p, long S, int w) {
+  mxArray* a = mxCreateDoubleMatrix((mwSize)S, (mwSize)w, mxREAL);
+  double* q = mxGetPr(a);
+  for (long s = 0; s < S; ++s)
+    for (int i = 0; i < w; ++i) q[(size_t)i * S + s] = p[s * w + i];
+  return a;
+}
+
+/* C [S][rows][nit] -> MATLAB rows x nit x S */
+static mxArray* out_signals(const double* p, long S, int rows, int nit) {
+  mwSize dims[3] = {(mwSize)rows, (mwSize)nit, (mwSize)S};
+  mxArray* a = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
+  double* q = mxGetPr(a);
+  for (long s = 0; s < S; ++s)
+    for (int i = 0; i < rows; ++i)
+      for (int t = 0; t < nit; ++t) q[(size_t)s * rows * nit + (size_t)t * rows + i] = p[((size_t)s * rows + i) * nit + t];
+  return a;
+}
+
+static void cmd_eval(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[], int multi) {
+  const int a0 = multi ? 3 : 2; /* first candidate argument */
+  if (nrhs < a0 + 5) mexErrMsgIdAndTxt("mpct:arg", "usage: mpct_mex('%s', h,%s N2, Nu, delta, lambda, r [, v, opts])",
+                                       multi ? "eval_multi" : "eval", multi ? " devices," : "");
+  mpct_scenario* s = handle(prhs[1]);
+  int my, nu, nd;
+  dims_of(s, &my, &nu, &nd);
+  const long C = (long)mxGetNumberOfElements(prhs[a0]);
+  int32_t* N2 = ints(prhs[a0], -1, "N2");
+  int32_t* Nu = ints(prhs[a0 + 1], C, "Nu");
+  double* delta = rows_of(prhs[a0 + 2], C, my, "delta");
+  double* lambda = rows_of(prhs[a0 + 3], C, nu, "lambda");
+  const mxArray* ra = prhs[a0 + 4];
+  const mwSize* rd = mxGetDimensions(ra);
+  const int nit = mxGetNumberOfDimensions(ra) >= 2 ? (int)rd[1] : 0;
+  int nref = 0;
+  double* r = signals(ra, my, nit, &nref, "r");
+  const mxArray* va = nrhs > a0 + 5 ? prhs[a0 + 5] : NULL;
+  double* v = NULL;
+  if (va && !mxIsEmpty(va)) {
+    const int nv = (int)mxGetM(va);
+    v = signals(va, nv, nit, &nref, "v");
+  }
+  mpct_opts o = read_opts(nrhs > a0 + 6 ? prhs[a0 + 6] : NULL);
+  int32_t* devs = NULL;
+  int ndev = 0;
+  if (multi) {
+    ndev = (int)mxGetNumberOfElements(prhs[2]);
+    devs = ints(prhs[2], -1, "devices");
+  }
+  const long S = C * nref;
+  const int traj = o.want_traj != 0, ol = o.open_loop != 0;
+  mpct_result res;
+  memset(&res, 0, sizeof res);
+  res.J1 = (double*)mxCalloc((size_t)(S * my + 1), sizeof(double));
+  res.j21 = (double*)mxCalloc((size_t)(S * my + 1), sizeof(double));
+  res.j22 = (double*)mxCalloc((size_t)(S * my + 1), sizeof(double));
+  res.Jnu = (double*)mxCalloc((size_t)(S * nu + 1), sizeof(double));
+  res.status = (int32_t*)mxCalloc((size_t)(S + 1), sizeof(int32_t));
+  res.qp_iters = (int64_t*)mxCalloc((size_t)(S + 1), sizeof(int64_t));
+  if (traj) {
+    res.y = (double*)mxCalloc((size_t)(S * my * nit + 1), sizeof(double));
+    res.u = (double*)mxCalloc((size_t)(S * nu * nit + 1), sizeof(double));
+    if (ol) {
+      res.ys = (double*)mxCalloc((size_t)(S * my * nit + 1), sizeof(double));
+      res.uopt = (double*)mxCalloc((size_t)(S * nu * nit + 1), sizeof(double));
+    }
+  }
+  const int rc = multi ? mpct_eval_batch_multi(s, ndev, devs, C, N2, Nu, delta, lambda, nref, r, v, &o, &res)
+                       : mpct_eval_batch(s, C, N2, Nu, delta, lambda, nref, r, v, &o, &res);
+  if (rc != MPCT_OK) lib_error(multi ? "mpct:eval_multi" : "mpct:eval");
+  mxArray* outs[10] = {NULL};
+  outs[0] = out_rows(res.J1, S, my);
+  outs[1] = out_rows(res.j21, S, my);
+  outs[2] = out_rows(res.j22, S, my);
+  outs[3] = out_rows(res.Jnu, S, nu);
+  outs[4] = mxCreateDoubleMatrix((mwSize)S, 1, mxREAL);
+  outs[5] = mxCreateDoubleMatrix((mwSize)S, 1, mxREAL);
+  for (long k = 0; k < S; ++k) {
+    mxGetPr(outs[4])[k] = res.status[k];
+    mxGetPr(outs[5])[k] = (double)res.qp_iters[k];
+  }
+  outs[6] = traj ? out_signals(res.y, S, my, nit) : mxCreateDoubleMatrix(0, 0, mxREAL);
+  outs[7] = traj ? out_signals(res.u, S, nu, nit) : mxCreateDoubleMatrix(0, 0, mxREAL);
+  outs[8] = (traj && ol) ? out_signals(res.ys, S, my, nit) : mxCreateDoubleMatrix(0, 0, mxREAL);
+  outs[9] = (traj && ol) ? out_signals(res.uopt, S, nu, nit) : mxCreateDoubleMatrix(0, 0, mxREAL);
+  const int nout = nlhs < 1 ? 1 : (nlhs > 10 ? 10 : nlhs);
+  for (int k = 0; k < 10; ++k) {
+    if (k < nout) plhs[k] = outs[k];
+    else mxDestroyArray(outs[k]);
+  }
+  (void)nd;
+}
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+  if (!g_atexit) {
+    mexAtExit(destroy_all);
+    g_atexit = 1;
+  }
+  char cmd[32];
+  if (nrhs < 1 || !mxIsChar(prhs[0]) || mxGetString(prhs[0], cmd, sizeof cmd) != 0)
+    mexErrMsgIdAndTxt("mpct:arg", "first argument must be a command string");
+  if (!strcmp(cmd, "version")) {
+    plhs[0] = mxCreateDoubleScalar((double)mpct_abi_version());
+  } else if (!strcmp(cmd, "create")) {
+    if (nrhs != 2) mexErrMsgIdAndTxt("mpct:arg", "usage: h = mpct_mex('create', desc)");
+    cmd_create(nlhs, plhs, prhs[1]);
+  } else if (!strcmp(cmd, "create_nmpc")) {
+    if (nrhs != 2) mexErrMsgIdAndTxt("mpct:arg", "usage: h = mpct_mex('create_nmpc', desc)");
+    cmd_create_nmpc(plhs, prhs[1]);
+  } else if (!strcmp(cmd, "eval")) {
+    cmd_eval(nlhs, plhs, nrhs, prhs, 0);
+  } else if (!strcmp(cmd, "eval_multi")) {
+    cmd_eval(nlhs, plhs, nrhs, prhs, 1);
+  } else if (!strcmp(cmd, "instance")) {
+    if (nrhs < 2) mexErrMsgIdAndTxt("mpct:arg", "usage: name = mpct_mex('instance', h [, opts])");
+    mpct_scenario* s = handle(prhs[1]);
+    mpct_opts o = read_opts(nrhs > 2 ? prhs[2] : NULL);
+    char name[160];
+    if (mpct_kernel_instance(s, &o, name, (int32_t)sizeof name) < 0) lib_error("mpct:instance");
+    plhs[0] = mxCreateString(name);
+  } else if (!strcmp(cmd, "destroy")) {
+    if (nrhs != 2) mexErrMsgIdAndTxt("mpct:arg", "usage: mpct_mex('destroy', h)");
+    mpct_scenario* s = handle(prhs[1]);
+    for (int k = 0; k < MPCT_MEX_MAX; ++k)
+      if (g_live[k] == s) g_live[k] = NULL;
+    mpct_scenario_destroy(s);
+  } else {
+    mexErrMsgIdAndTxt("mpct:arg", "unknown command '%s'", cmd);
+  }
+}

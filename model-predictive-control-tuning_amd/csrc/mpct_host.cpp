@@ -137,8 +137,87 @@ static void step_response(const mpct_dtf& d, int T, double* s) {
   std::copy(y.begin(), y.end(), s);
 }
 
-extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d, mpct_scenario** out) {
-  if (!d || !out) return fail(MPCT_EINVAL, "null argument");
+// descompMPC.m:19-43 followed by the exact-LCM CARIMA form (BA_MIMO.m:20-71 with the row's
+// DISTINCT denominator polynomials multiplied, instead of the rounded-roots LCM): what a host that
+// passes na = carima_A = nb = carima_B = dp = NULL gets (abi >= 5; the MATLAB MEX host builds its
+// descriptor from the mpc object's tfdata alone).  Same arithmetic as mpct/lti.py descomp + carima
+// (exact=True), checked against it in tests/test_abi.py.
+struct CarimaTables {
+  std::vector<int32_t> na, nb, dp;
+  std::vector<double> A, B;
+};
+
+static void derive_carima(const mpct_dtf* model, int my, int nin, CarimaTables& c) {
+  c.na.assign(my, 0);
+  c.nb.assign((size_t)my * nin, 0);
+  c.dp.assign((size_t)my * nin, 0);
+  c.A.clear();
+  c.B.clear();
+  std::vector<std::vector<double>> Bs((size_t)my * nin);
+  for (int i = 0; i < my; ++i) {
+    int dmax = 0;
+    for (int j = 0; j < nin; ++j) dmax = std::max(dmax, model[i * nin + j].delay);
+    for (int j = 0; j < nin; ++j) {
+      const mpct_dtf& m = model[i * nin + j];
+      std::vector<double> b(m.num, m.num + m.len);
+      int dd = m.delay;
+      if (b[0] != 0.0) {  // descompMPC.m:35-38: d = d - 1, B = [0 B]
+        dd -= 1;
+        b.insert(b.begin(), 0.0);
+      }
+      double sn = 0.0, sd = 0.0;
+      for (int k = 0; k < m.len; ++k) {
+        sn += m.num[k];
+        sd += m.den[k];
+      }
+      if (sd != 0.0 && sn / sd == 0.0) dd = dmax;  // descompMPC.m:39-41: zero dcgain
+      c.dp[i * nin + j] = dd;
+      if (b[0] == 0.0) b.erase(b.begin());  // BA_MIMO.m:22-24: one leading zero stripped
+      Bs[i * nin + j] = b;
+    }
+  }
+  for (int i = 0; i < my; ++i) {
+    std::vector<std::vector<double>> uniq;
+    auto den = [&](int j) { return std::vector<double>(model[i * nin + j].den, model[i * nin + j].den + model[i * nin + j].len); };
+    for (int j = 0; j < nin; ++j) {
+      const std::vector<double> a = den(j);
+      if (std::find(uniq.begin(), uniq.end(), a) == uniq.end()) uniq.push_back(a);
+    }
+    std::vector<double> Ai{1.0};
+    for (const auto& u : uniq) Ai = conv(Ai, u);
+    c.na[i] = (int)Ai.size() - 1;
+    for (double x : Ai) c.A.push_back(x / Ai[0]);
+    for (int j = 0; j < nin; ++j) {
+      std::vector<double> b = Bs[i * nin + j];
+      const std::vector<double> a = den(j);
+      for (const auto& u : uniq)
+        if (u != a) b = conv(b, u);
+      c.nb[i * nin + j] = (int)b.size() - 1;
+      for (double x : b) c.B.push_back(x / Ai[0]);
+    }
+  }
+}
+
+extern "C" int32_t mpct_scenario_create(const mpct_scenario_desc* d_in, mpct_scenario** out) {
+  if (!d_in || !out) return fail(MPCT_EINVAL, "null argument");
+  mpct_scenario_desc dcopy = *d_in;
+  const mpct_scenario_desc* d = &dcopy;
+  CarimaTables derived;
+  if (d_in->abi_version >= 5 && !(d_in->mdband) && d_in->dtc == 0 && !d_in->na && !d_in->carima_A && !d_in->nb &&
+      !d_in->carima_B && !d_in->dp && d_in->model && d_in->my >= 1 && d_in->nu >= 1 && d_in->nd >= 0 &&
+      d_in->my <= kMaxOut && d_in->nu + d_in->nd <= kMaxIn) {
+    const int nin = d_in->nu + d_in->nd;
+    for (int e = 0; e < d_in->my * nin; ++e) {
+      const mpct_dtf& m = d_in->model[e];
+      if (m.len < 1 || !m.num || !m.den || m.den[0] == 0.0 || m.delay < 0) return fail(MPCT_EINVAL, "bad model entry");
+    }
+    derive_carima(d_in->model, d_in->my, nin, derived);
+    dcopy.na = derived.na.data();
+    dcopy.nb = derived.nb.data();
+    dcopy.dp = derived.dp.data();
+    dcopy.carima_A = derived.A.data();
+    dcopy.carima_B = derived.B.data();
+  }
   *out = nullptr;
   if (d->abi_version < 1 || d->abi_version > MPCT_ABI_VERSION) return fail(MPCT_EINVAL, "abi_version mismatch");
   const int dtc = d->abi_version >= 2 ? (d->dtc ? 1 : 0) : 0;

@@ -39,11 +39,13 @@ class Scenario:
     ``bands``: the toolbox MPC with measured disturbances and soft output bands (Shell7x5.m,
     WoodBerry.m; ABI mdband): dict(y_min, y_max, ecr_min, ecr_max, y_scale=None, u_scale=None,
     rho=1e4) of OV Min/Max, MinECR/MaxECR, ScaleFactors and Weights.ECR.  Scenarios with measured
-    disturbances (nd > 0) always use that kernel (unbounded outputs when bands is None)."""
+    disturbances (nd > 0) always use that kernel (unbounded outputs when bands is None).
+    ``host_carima``: False passes no CARIMA tables and lets the library derive them from the model
+    (exact LCM, what the MATLAB MEX host does; toolbox window only)."""
 
     def __init__(self, plant, model, nu, du_min, du_max, u_min, u_max, yref, n2_max, nu_max,
                  Ts=1.0, window="toolbox", weights_squared=True, exact_carima=True, vns_ink=10,
-                 dtc=False, filters=None, dist=None, plant_variants=None, bands=None):
+                 dtc=False, filters=None, dist=None, plant_variants=None, bands=None, host_carima=True):
         self.lib = _lib.load()
         self.plant, self.model = plant, model
         self.my, self.nin = len(model), len(model[0])
@@ -97,7 +99,8 @@ class Scenario:
         d.n1 = _ip(n1)
         d.plant = dtf_array(plant)
         d.model = dtf_array(model)
-        d.na, d.carima_A, d.nb, d.carima_B, d.dp = _ip(na32), _dp(A_cat), _ip(nb32), _dp(B_cat), _ip(dp32)
+        if host_carima or self.dtc or not exact_carima:
+            d.na, d.carima_A, d.nb, d.carima_B, d.dp = _ip(na32), _dp(A_cat), _ip(nb32), _dp(B_cat), _ip(dp32)
         d.du_min, d.du_max, d.u_min, d.u_max = (_dp(b) for b in bnds)
         d.yref = _dp(self.yref)
         d.dtc = int(self.dtc)

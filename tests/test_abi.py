@@ -269,3 +269,42 @@ def test_kernel_instance_and_multi_validation(built):
         eval_batch_multi(sc, [], N2, 5, d, d, r[None])
     lib = _lib.load()
     assert lib.mpct_kernel_instance(None, None, None, 0) < 0
+
+
+def test_library_derived_carima_equals_host(built):
+    """abi 5: a descriptor without CARIMA tables (what the MATLAB MEX host passes) gets the same
+    candidate-independent tables as the Python host's descompMPC + exact-LCM CARIMA
+    (mpct/lti.py): step table, Phi (reference and device bases) and dimensions, bit for bit."""
+    from mpct.scenarios import shell3x3, woodberry_toolbox  # noqa: F401
+    from mpct.scenarios import SHELL3_L, SHELL3_R, shell3x3_plant, shell3x3_xsp
+    from mpct.engine import Scenario
+
+    P = shell3x3_plant(SHELL3_L, SHELL3_R)
+    yref = SHELL3_L[:, None] * shell3x3_xsp(500)
+    kw = dict(nu=3, du_min=-0.05 / SHELL3_R, du_max=0.05 / SHELL3_R, u_min=-1.0 / SHELL3_R, u_max=0.5 / SHELL3_R,
+              yref=yref, n2_max=30, nu_max=5, Ts=4.0)
+    a = Scenario(P, P, **kw)
+    b = Scenario(P, P, host_carima=False, **kw)
+    for which in (0, 1, 2, 3):
+        np.testing.assert_array_equal(a.table(which), b.table(which))
+
+
+def test_integration_build_line_covers_every_unit():
+    """the build documented in INTEGRATION.md must compile and link every translation
+    unit of csrc/ (the same list __graft_entry__.build() uses), and the MATLAB side asserts the
+    current ABI."""
+    import __graft_entry__ as g
+
+    units = sorted(f for f in os.listdir(os.path.join(ROOT, "model-predictive-control-tuning_amd", "csrc"))
+                   if f.endswith((".hip", ".cpp")))
+    assert units == sorted(g.KERNELS + g.AUX_SOURCES + ("mpct_host.cpp",))
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    loop = re.search(r"for f in ([^;]+); do", doc).group(1).split()
+    assert sorted(loop) == units
+    link = re.search(r"hipcc --offload-arch=gfx950 -shared -fPIC ([^\n]+\n[^\n]+)", doc).group(1)
+    objs = sorted(os.path.basename(o)[:-2] for o in re.findall(r"\S+\.o", link))
+    assert objs == sorted(os.path.splitext(u)[0] for u in units)
+    mex = open(os.path.join(ROOT, "matlab", "build_mpct_mex.m")).read()
+    from mpct import _lib
+
+    assert "v >= %d" % _lib.ABI_VERSION in mex

@@ -349,8 +349,10 @@ def test_nonsquare_vns_objective_shell7x5(gpu):
         np.testing.assert_allclose(j22[k], o22, rtol=COST_RTOL)
         ok = onu < 1e6
         np.testing.assert_allclose(jnu[k][ok], onu[ok], rtol=1e-5)
-        Fo = o21.sum() + o22.sum() + c[0] + onu.sum()
-        assert abs(F[k] - Fo) <= 1e-5 * abs(Fo), (k, F[k], Fo)
+        # F = sum(j21 + j22) + N(1) + sum(Jnu); a Jnu term divides by |diff(uopt)|, which is a
+        # rounding-level difference when two moves sit on the same bound (Jnu ~ 1e30 on both
+        # sides, no digits in common): the comparison keeps the well-conditioned part
+        np.testing.assert_allclose(F[k] - jnu[k].sum(), o21.sum() + o22.sum() + c[0], rtol=COST_RTOL)
 
 
 @pytest.mark.gpu
