@@ -123,9 +123,11 @@ def _oracle_compare(res, C, D, N2, Nu, d, l, pairs, plants):
         s = c * D + k
         p, m = int(N2[c]), int(Nu[c])
         ref = dtc_gpc_ww(p=(p, p), m=(m, m), lam=tuple(l[c]), delta=tuple(d[c]), plant=plants[k])
-        if not np.all(np.isfinite(ref["y"])) or np.max(np.abs(ref["y"])) > 1e6:
-            assert res.status[s] & 4, (c, k, res.status[s])  # the draw destabilises the loop on both sides
+        if not np.all(np.isfinite(ref["y"])):
+            assert res.status[s] & 4, (c, k, res.status[s])  # overflow on both sides
             continue
+        # a draw that destabilises the loop (|y| up to 1e86 on this grid) is still compared: the
+        # divergent trajectories agree to the same relative accuracy
         assert res.status[s] == 0, (c, k, res.status[s])
         ey, eu = _trel(res.y[s], ref["y"]), _trel(res.u[s], ref["u"])
         J1 = np.sum((ref["y"] - ref["r"]) ** 2, axis=1)
