@@ -45,6 +45,74 @@ def algorithmic_flops_per_sim(sc, N2, Nu, iters_per_step):
     return setup + sc.nit * per_step
 
 
+def band_flops_per_sim(sc, N2, Nu, iters):
+    """Algorithmic flops of one config-3 simulation (mdband_kernel.hip): per step the
+    free-response window update 2*P*nin (P = my*N2 output rows, nin = MVs + MDs), the feasibility
+    scan of the 2P soft output rows against the M+1 QP variables 2*(2P)*(M+1), and per Goldfarb-
+    Idnani iteration another scan plus the factor update 2*(2P)*(M+1) + 6*(M+1)^2; setup: the
+    column-streamed QR of the M+1 weighted rows 2*(M+1)^3/3.  iters = measured GI iterations."""
+    P, M1 = sc.my * N2, sc.nu * Nu + 1
+    per_step = 2 * P * sc.nin + 4 * P * M1
+    return 2 * M1 ** 3 / 3.0 + sc.nit * per_step + iters * (4 * P * M1 + 6 * M1 * M1)
+
+
+def nmpc_flops_per_sim(N, Nu, gn_iters, nit=60, nsub=10, nx=3, ny=2, nu=2):
+    """Algorithmic flops of one config-5 simulation (nmpc_kernel.hip), per Gauss-Newton
+    iteration: the RK4 prediction over N steps x nsub sub-steps x 4 stages of the model (~40 flops)
+    and of its M+1 forward tangents (2*nx^2 each), the streamed QR of the N*ny output rows into M+1
+    columns (3*(M+1)^2 per row), an Armijo trial pass (prediction only); per closed-loop step the
+    plant's own RK4 integration.  gn_iters = measured Gauss-Newton iterations of the simulation."""
+    M1 = nu * Nu + 1
+    rk = N * nsub * 4
+    per_gn = rk * (40 + 2 * nx * nx * M1) + N * ny * 3 * M1 * M1 + rk * 40
+    return gn_iters * per_gn + nit * nsub * 4 * 40
+
+
+def cpu_share():
+    """(cpus, note): the CPUs this process may use -- its affinity set, limited by a cgroup CPU
+    quota when one is set (the GPU box gives each GPU a share of the host)."""
+    n = len(os.sched_getaffinity(0))
+    note = "%d CPUs in the affinity set" % n
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            note += ", cgroup quota %d CPUs" % quota
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return n, note
+
+
+def reference_structured_baseline(N2v, Nuv, d, l, J1, seconds):
+    """Config 2, reference-structured, 1 thread: the numpy restatement of
+    closedloop_toolbox with the plant re-simulated over the whole input history every step
+    (lsim, DTC_GPC_WW.m:130-136 structure, O(nit^2)) and the primal active-set QP, on seeded
+    random candidates of the same grid for ~`seconds`."""
+    from oracle.scenarios import shell3x3 as o_shell3x3
+    from oracle.toolbox_gpc import closedloop_toolbox as o_cl
+
+    osc, orr, oyref, _ = o_shell3x3()
+    done, tc, rel = 0, 0.0, []
+    for k in np.random.default_rng(20250307).permutation(len(N2v)):
+        k = int(k)
+        t1 = time.perf_counter()
+        o = o_cl(osc, orr, None, int(N2v[k]), int(Nuv[k]), d[k], l[k], orr.shape[1], open_loop=False,
+                 full_history=True)
+        tc += time.perf_counter() - t1
+        done += 1
+        j = ((o.y - oyref) ** 2).sum(1)
+        rel.append(float(np.max(np.abs(J1[k] - j) / np.abs(j))))
+        if tc >= seconds:
+            break
+    return {"value": done / tc, "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": "oracle/toolbox_gpc.py closedloop_toolbox(full_history=True): numpy, plant re-simulated "
+                      "with lsim over the whole history every step (DTC_GPC_WW.m:130-136 structure), primal "
+                      "active-set QP; %d seeded random candidates of the metric grid, 1 thread, %.1f s; max rel "
+                      "|J1_gpu - J1_cpu| = %.1e" % (done, tc, max(rel))}
+
+
 def other_cpu_baseline(workload, N2, Nu, d, l, refs, J1, st, seconds):
     """Single-thread CPU restatement (oracle/) of a config-3/4/5 simulation, timed on a bounded
     seeded sample of the same grid (rank 0, N = 1): the reference-structured numpy loops, i.e.
@@ -125,6 +193,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="thread-seconds of CPU baseline work")
+    ap.add_argument("--ref-seconds", type=float, default=10.0,
+                    help="seconds of the reference-structured single-thread CPU leg (0: skip)")
     ap.add_argument("--workload", default="shell3x3", choices=("shell3x3", "shell7x5", "vandevusse", "dtc-mc"),
                     help="shell3x3 = the BASELINE metric (config 2); the others are SURVEY §8d configs 3, 5, 4")
     args = ap.parse_args()
@@ -205,6 +275,9 @@ def main():
     value = sims / elapsed
     fl = algorithmic_flops_per_sim(sc, args.n2, args.nu, I_as) * C
     achieved = fl / (kms * 1e-3) / 1e12
+    from mpct.engine import kernel_instance
+
+    kernel_name = kernel_instance(sc)
 
     # PCIe-inclusive rate of the host-buffer entry point (mpct_eval_batch: H2D candidates,
     # kernel, D2H costs), after the timed region; reported beside `value`, never as `value`
@@ -241,8 +314,8 @@ def main():
 
         osc, orr, oyref, _ = o_shell3x3()
         cp = CPort(osc, args.n2, sc.nit, oyref)
-        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        threads = max(1, min(threads, 64))
+        share, share_note = cpu_share()
+        threads = max(1, args.cpu_threads or share)
         ncpu = C
         # bounded sample: repeat passes over the same batch until ~args.cpu_seconds of CPU work
         passes, tc = 0, 0.0
@@ -255,12 +328,19 @@ def main():
                 break
         gpuJ = out["J1"].cpu().numpy()[:ncpu]
         rel = float(np.max(np.abs(gpuJ - ref["J1"]) / np.maximum(np.abs(ref["J1"]), 1e-12)))
-        cpu = {"value": passes * ncpu / tc, "unit": "sims/s", "cores": threads, "kind": "port",
-               "sample": "oracle/cgpc.c on the same %d-candidate Shell 3x3 batch (N2=%d, Nu=%d, nit=500), "
-                         "%d passes, %d OpenMP threads, %.2f s wall (%.0f thread-s); max rel "
-                         "|J1_gpu - J1_cpu| = %.1e; host %s, %d logical CPUs visible"
-                         % (ncpu, args.n2, args.nu, passes, threads, tc, tc * threads, rel, cpu_model(),
-                            os.cpu_count() or 0)}
+        rate = passes * ncpu / tc
+        cpu = {"value": rate, "unit": "sims/s", "cores": threads, "kind": "port",
+               "per_core": rate / threads,
+               "sample": "oracle/cgpc.c (C restatement, incremental recursions, same QR / dual active-set "
+                         "arithmetic) on the same %d-candidate Shell 3x3 batch (N2=%d, Nu=%d, nit=500), %d passes, "
+                         "%d OpenMP threads = every CPU this process may use (%s), %.2f s wall (%.0f thread-s), "
+                         "%.0f sims/s per core; max rel |J1_gpu - J1_cpu| = %.1e; host %s, %d logical CPUs in "
+                         "the machine" % (ncpu, args.n2, args.nu, passes, threads, share_note, tc, tc * threads,
+                                          rate / threads, rel, cpu_model(), os.cpu_count() or 0)}
+
+    cpu_ref = None
+    if not args.no_cpu_baseline and world == 1 and args.ref_seconds > 0:
+        cpu_ref = reference_structured_baseline(N2, Nu, d, l, out["J1"].cpu().numpy(), args.ref_seconds)
 
     line = {
         "metric": "closed-loop GPC sims/sec (Shell 3x3, N2=30 Nu=5) over tuning grid",
@@ -280,11 +360,14 @@ def main():
                                "RCCL all-gather + ranking" % C,
                    "candidates_per_gpu": C, "N2": args.n2, "Nu": args.nu, "nit": sc.nit,
                    "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "gpc_closed_loop_kernel", "kernel_ms": kms,
-                     "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as},
+                     "kernel": kernel_name, "kernel_ms": kms,
+                     "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as,
+                     "bound_note": "FP64 vector ALU issue + per-step dependent latency (no MFMA on this path: "
+                                   "DESIGN §6); peak = MI355X FP64 vector dense peak"},
         "cpu_baseline": cpu,
+        "cpu_baseline_reference_structured": cpu_ref,
         "host_api_sims_per_s": host_rate,
         "status_nonzero": nbad,
         "top_candidate": int(order[0].item()),
@@ -398,6 +481,35 @@ def other_workload(args):
         elapsed = float(te.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     st = out["status"].cpu().numpy()
+    iters = out["qp_iters"].cpu().numpy()
+    # algorithmic flops of the launch(es) over this rank's simulations (DESIGN §7 models)
+    cN2 = np.repeat(sN2, nref).astype(np.int64)
+    cNu = np.repeat(sNu, nref).astype(np.int64)
+    live = cN2 > 0
+    n_, u_, i_ = cN2[live].astype(float), cNu[live].astype(float), iters[live].astype(float)
+    if args.workload == "shell7x5":
+        fl = float(np.sum(band_flops_per_sim(sc, n_, u_, i_)))
+        kname, ibound = "mdband_closed_loop_kernel (class launches)", "GI iterations"
+    elif args.workload == "vandevusse":
+        fl = float(np.sum(nmpc_flops_per_sim(n_, u_, i_, nit=sc.nit)))
+        kname, ibound = "nmpc_closed_loop_kernel (class launches)", "Gauss-Newton iterations"
+    else:
+        # linear in the QP iterations: f(N2, Nu, 0) per horizon pair + 6 M^2 per iteration
+        fl = 0.0
+        for n, u in set(zip(cN2[live].tolist(), cNu[live].tolist())):
+            sel = (cN2[live] == n) & (cNu[live] == u)
+            fl += sel.sum() * algorithmic_flops_per_sim(sc, n, u, 0.0) + 6.0 * (sc.nu * u) ** 2 * i_[sel].sum()
+        from mpct.engine import kernel_instance
+
+        kname, ibound = kernel_instance(sc), "QP iterations"
+    achieved = fl / (kms * 1e-3) / 1e12
+    roof = {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kname, "kernel_ms": kms,
+            "algorithmic_gflop_per_launch": fl / 1e9,
+            "iterations_per_sim": float(iters[live].mean()) if live.any() else 0.0,
+            "bound_note": "FP64 vector ALU + per-step latency; flops from the DESIGN §7 model with the "
+                          "measured %s of every simulation; kernel_ms = HIP events around the whole "
+                          "eval call (all class launches)" % ibound}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = other_cpu_baseline(args.workload, N2, Nu, d, l, refs, out["J1"].cpu().numpy(), st,
@@ -408,7 +520,7 @@ def other_workload(args):
                 "warmup": warm, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f64", "data": "synthetic candidate grid (seed 20250307) on the "
                 "reference's scenario", "config": dict(cfg, parallelism="dp%d" % world),
-                "roofline": None, "kernel_ms_rank0": kms, "cpu_baseline": cpu,
+                "roofline": roof, "kernel_ms_rank0": kms, "cpu_baseline": cpu,
                 "status_codes": {int(k): int(n) for k, n in zip(*np.unique(st, return_counts=True))},
                 "top_candidate": int(order[0].item())}
         print(json.dumps(line), flush=True)

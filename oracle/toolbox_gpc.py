@@ -249,11 +249,14 @@ class _Plant:
 
 
 def closedloop_toolbox(sc: Scenario, r, v, N2: int, Nu: int, delta, lam, nit: int,
-                       open_loop: bool = True) -> CLResult:
+                       open_loop: bool = True, full_history: bool = False) -> CLResult:
     """[y,u,t,ys,uopt] = closedloop_toolbox(mpc,r,v,N,Nu,delta,lambda,nit) restated.
 
     r: my x nit reference (row signals, as the callers pass Xsp), v: nd x nit (may be empty).
     Returns row-signal arrays (my x nit, nu x nit) like col2row at closedloop_toolbox.m:103-107.
+    full_history: the plant output of step t is re-simulated over the whole input history with
+    lsim (scipy lfilter per entry), the structure of DTC_GPC_WW.m:130-136 / OptimalPredictor2.m:
+    28-37 -- O(nit^2) per simulation, the reference-structured CPU baseline.
     """
     my, nu, nd = sc.my, sc.nu, sc.nd
     r = np.asarray(r, dtype=float).reshape(my, nit)
@@ -308,8 +311,15 @@ def closedloop_toolbox(sc: Scenario, r, v, N2: int, Nu: int, delta, lam, nit: in
     u_prev = np.zeros(nu)
     iters = 0
     DU = np.zeros((nu, nit))
+    if full_history:
+        from scipy.signal import lfilter
+
     for t in range(nit):
-        yt = plant.output_at(U, t, ystate)
+        if full_history:   # y = lsim(P, u(1:k)) every step (DTC_GPC_WW.m:130-131)
+            yt = np.array([sum(lfilter(*plant.ba[i][j], U[j, :t + 1])[t] for j in range(sc.nin))
+                           for i in range(my)])
+        else:
+            yt = plant.output_at(U, t, ystate)
         Y[:, t] = yt
         for i in range(my):
             yhist[i] = np.concatenate([[yt[i]], yhist[i][:-1]])
