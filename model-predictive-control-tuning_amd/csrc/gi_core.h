@@ -122,11 +122,48 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
   return rk;
 }
 
-// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
+// Explicit B = R_A^-1 (row-major, stride M, leading q x q block valid), an optional companion of
+// R_A: the dual direction r = R_A^-1 d and the warm start's R_A'w = c, lambda = R_A^-1 w become
+// lane-parallel dot products instead of q-step serial substitutions (each step a v_readlane
+// broadcast and an LDS read).  An add appends column q (-r / alpha, 1 / alpha; row q zero left of
+// the diagonal), a drop rotates columns jj, jj+1 with the Givens rotations of R_A's rows and
+// removes row kd, since (G R_A E)^-1 = rows != kd of (R_A^-1 G').  Rebuilt with J.
+// r_w = sum_{c<q} B(w,c) v_c  (lane w < q; v in LDS, synchronised by the caller)
+__device__ __forceinline__ double gi_bdot(const double* sB, const double* sv, int q, int M) {
+  const int lane = threadIdx.x;
+  double a0 = 0.0, a1 = 0.0;
+  if (lane < q) {
+    const double* b = sB + lane * M;
+    int c = lane;  // upper triangular
+    for (; c + 1 < q; c += 2) {
+      a0 += b[c] * sv[c];
+      a1 += b[c + 1] * sv[c + 1];
+    }
+    if (c < q) a0 += b[c] * sv[c];
+  }
+  return a0 + a1;
+}
+// w_k = sum_{w<=k} B(w,k) v_w  (lane k < q): B'v
+__device__ __forceinline__ double gi_btdot(const double* sB, const double* sv, int q, int M) {
+  const int lane = threadIdx.x;
+  double a0 = 0.0, a1 = 0.0;
+  if (lane < q) {
+    int w = 0;
+    for (; w + 1 <= lane; w += 2) {
+      a0 += sB[w * M + lane] * sv[w];
+      a1 += sB[(w + 1) * M + lane] * sv[w + 1];
+    }
+    if (w <= lane) a0 += sB[w * M + lane] * sv[w];
+  }
+  return a0 + a1;
+}
+
+// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:));
+// with sB: rk = (R_A^-1 d(0:q))_lane on lanes < q
 template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
-                                       const Mark& mark) {
+                                       const Mark& mark, double* sB = nullptr, double rk = 0.0) {
   const int lane = threadIdx.x;
   const int q = S.q;
   const double dq = bcast(dk, q);
@@ -141,11 +178,19 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
   if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  const double ia = 1.0 / alpha;
   if (lane == q) {
     sRA[q * M + q] = alpha;
-    S.rdg = 1.0 / alpha;
+    S.rdg = ia;
     S.uw = upm;
     S.ww = p;
+  }
+  if (sB) {
+    if (lane < q) {
+      sB[lane * M + q] = -rk * ia;
+      sB[q * M + lane] = 0.0;
+    }
+    if (lane == q) sB[q * M + q] = ia;
   }
   mark(S, p, true);
   S.q = q + 1;
@@ -156,7 +201,7 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
 template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
-                                        const Mark& mark) {
+                                        const Mark& mark, double* sB = nullptr) {
   const int lane = threadIdx.x;
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
@@ -191,10 +236,18 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
           sJT[jj * M + lane] = cs * j0v + sn * j1v;
           sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
         }
+        if (sB && lane < q) {  // B G': columns jj, jj+1 (lanes = rows)
+          const double b0 = sB[lane * M + jj], b1 = sB[lane * M + jj + 1];
+          sB[lane * M + jj] = cs * b0 + sn * b1;
+          sB[lane * M + jj + 1] = -sn * b0 + cs * b1;
+        }
         S.nrot += 1;
       }
       lds_sync();
     }
+  }
+  if (sB && lane < q - 1) {  // row kd of B G' leaves (lanes = columns)
+    for (int w = kd; w < q - 1; ++w) sB[w * M + lane] = sB[(w + 1) * M + lane];
   }
   const int qn = q - 1;
   if (lane == qn) {

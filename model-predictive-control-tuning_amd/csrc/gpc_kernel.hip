@@ -23,6 +23,7 @@
 
 #include "mpct_dev.h"
 #include "gi_core.h"
+#include "gpc_qp.h"
 
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
@@ -37,8 +38,8 @@
 namespace mpct {
 
 struct LdsLayout {
-  int rinv, jt, dv, ra, sl, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb, mza,
-      frb, fra, total;
+  int rinv, jt, dv, ra, sl, gb, gw, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb,
+      mza, frb, fra, total;
 };
 
 // LDS layout of one simulation; [x, plb) holds the state and every history (zeroed at start)
@@ -54,6 +55,8 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   L.dv = take(M);            // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
+  L.gb = take(MPCT_GI_B ? M * M : 0);  // B = R_A^-1 (row-major)
+  L.gw = take(MPCT_GI_B ? M : 0);      // warm start: w = R_A^-T c
   L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
   L.x = take(nx + 1);
   L.xc = take(M);
@@ -94,201 +97,6 @@ __device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m
     s[3] = (rc.umax - up) - pre;
   }
 }
-
-// normal of constraint p = 4m + kind: rows j0..m of the MV block, sign
-__device__ __forceinline__ void gi_normal(int p, const RowCons& rc, int& j0, int& mp, double& sg) {
-  mp = p >> 2;
-  const int kind = p & 3;
-  j0 = kind < 2 ? mp : mp - __builtin_amdgcn_readlane(rc.l, mp);
-  sg = (kind & 1) ? -1.0 : 1.0;
-}
-
-template <int MAXM>
-__device__ __forceinline__ int gi_qp(double* __restrict__ lds, const LdsLayout& L, int M, int Nu, const RowCons& rc,
-                     double xu, double tol, int maxit, int* st, GIState<MAXM>& S
-#ifdef MPCT_PROFILE
-                     , unsigned long long* pacc, unsigned long long& pprev
-#endif
-                     ) {
-  const int lane = threadIdx.x;
-  const bool row = lane < M;
-  const double* sRi = lds + L.rinv;
-  double* sxc = lds + L.xc;
-  double* sJT = lds + L.jt;
-  double* sd = lds + L.dv;
-  double* sRA = lds + L.ra;
-  double* ssl = lds + L.sl;
-  const double* suprev = lds + L.uprev;
-  const double up_row = row ? suprev[rc.n] : 0.0;
-  const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
-  auto slacks = [&](double x, double s[4]) {
-    const double pre = block_prefix<MAXM>(x, rc.l, Nu, row, sxc);
-    if (rc.l == 0) {
-      s[0] = x - lo_box;
-      s[1] = hi_box - x;
-      s[2] = INFINITY;
-      s[3] = INFINITY;
-    } else {
-      s[0] = x - rc.dmin;
-      s[1] = rc.dmax - x;
-      s[2] = pre - (rc.umin - up_row);
-      s[3] = (rc.umax - up_row) - pre;
-    }
-    if (!row) s[0] = s[1] = s[2] = s[3] = INFINITY;
-  };
-  int it = 0;
-  double xm = xu;
-  {
-    // the unconstrained minimiser is optimal when it is feasible (the retained set is kept)
-    double s[4];
-    slacks(xu, s);
-    const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
-    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
-    if (S.q == 0) {
-      S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
-    } else {
-      if (row) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
-      }
-      if (!S.jinit || S.nrot >= 4 * M) {
-        // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
-        const int qq = S.q;
-        gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
-        S.q = 0;
-        for (int v = 0; v < qq; ++v) {
-          const int p = __builtin_amdgcn_readlane(S.ww, v);
-          int j0, mp;
-          double sg;
-          gi_normal(p, rc, j0, mp, sg);
-          const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sg, row);
-          const double beta = qsum<MAXM>(lane >= v ? dk * dk : 0.0);
-          lds_sync();
-          const double zm = gi_z(sJT, sd, v, M, row);
-          const double uk = S.uw;
-          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row, BoxMark{});
-          if (lane == v) S.uw = uk;
-          ++it;
-        }
-        S.nrot = 0;
-      }
-      lds_sync();
-      // equality-constrained solve on the retained set, dropping negative multipliers
-      for (;;) {
-        const int q = S.q;
-        if (q == 0) {
-          xm = xu;
-          break;
-        }
-        double c = 0.0;
-        if (lane < q) c = -ssl[S.ww];  // b_A - N_A'x_u
-        double wv = 0.0;
-        xm = xu;
-        for (int v = 0; v < q; ++v) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
-          const double w = bcast(c * S.rdg, v);
-          if (lane == v) wv = w;
-          if (lane > v && lane < q) c -= sRA[v * M + lane] * w;
-          if (row) xm += sJT[v * M + lane] * w;
-        }
-        const double lam = gi_backsub<MAXM>(S, sRA, M, wv);
-        if (lane < q) S.uw = lam;
-        double lmin = lane < q ? lam : INFINITY;
-        int kd = lane;
-        qargmin<MAXM>(lmin, kd);
-        if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{});
-        ++it;
-      }
-      if (!row) xm = 0.0;
-    }
-  }
-  PSTAMP(PROF_QWARM);
-#ifdef MPCT_DEBUG_SIM
-  if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0) printf("QP entry-after-warm q=%d it=%d nrot=%d\n", S.q, it, S.nrot);
-#endif
-  for (;;) {
-    // ---- most violated inactive constraint
-    double best = INFINITY;
-    int bid = 0x7fffffff;
-    {
-      double s[4];
-      slacks(xm, s);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (!((S.act >> k) & 1u) && s[k] < best) {
-          best = s[k];
-          bid = 4 * lane + k;
-        }
-    }
-    qargmin<MAXM>(best, bid);
-    PSTAMP(PROF_QCHECK);
-    if (!(best < -tol)) break;
-    if (it >= maxit || S.q >= M) {
-      *st |= MPCT_ST_QP_MAXITER_;
-      break;
-    }
-    if (!S.jinit) gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
-    const int p = bid;
-    int j0, mp;
-    double sgp;
-    gi_normal(p, rc, j0, mp, sgp);
-    double sp = best;  // slack of p along the path
-    double upm = 0.0;  // its multiplier
-    bool infeas = false;
-    for (;;) {
-      ++it;
-      const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sgp, row);
-      const double d2 = dk * dk;
-      const double dn2 = qsum<MAXM>(d2);
-      const double beta = qsum<MAXM>(lane >= S.q ? d2 : 0.0);
-      lds_sync();
-      const double zm = gi_z(sJT, sd, S.q, M, row);
-      PSTAMP(PROF_QD);
-      const double rk = gi_backsub<MAXM>(S, sRA, M, dk);
-      // dual step over active constraints with r_w > 0
-      double t1 = INFINITY;
-      int kdrop = 0x7fffffff;
-      if (lane < S.q && rk > 0.0) {
-        t1 = S.uw / rk;
-        kdrop = lane;
-      }
-      qargmin<MAXM>(t1, kdrop);
-      PSTAMP(PROF_QR);
-      const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
-      if (t1 == INFINITY && t2 == INFINITY) {
-        *st |= MPCT_ST_QP_INFEAS_;
-        infeas = true;
-        break;
-      }
-      const bool full = t2 <= t1;
-      const double t = full ? t2 : t1;
-#ifdef MPCT_DEBUG_SIM
-      if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0 && it > 40 && it < 70)
-        printf("it=%d q=%d p=%d sp=%.3e beta=%.3e dn2=%.3e t1=%.3e t2=%.3e kd=%d %s\n", it, S.q, p, sp, beta, dn2, t1, t2, kdrop, full ? "ADD" : "DROP");
-#endif
-      if (t2 != INFINITY) xm += t * zm;
-      if (lane < S.q) S.uw -= t * rk;
-      upm += t;
-      sp += t * beta;
-      if (full) {
-        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
-        PSTAMP(PROF_QADD);
-        break;
-      }
-      gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{});
-      PSTAMP(PROF_QDROP);
-      if (it >= maxit) {
-        *st |= MPCT_ST_QP_MAXITER_;
-        break;
-      }
-    }
-    if (it >= maxit || infeas) break;
-  }
-  if (row) sxc[lane] = xm;
-  lds_sync();
-  return it;
-}
-
 
 // EXT: the open-loop prediction and/or trajectories may be requested; the EXT = false instance
 // (GAM scoring: costs only) carries none of their state through the step loop
@@ -571,7 +379,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     lds_sync();
     PSTAMP(PROF_UNC);
 #ifndef MPCT_EXP_NOQP
-    iters += gi_qp<MAXM>(lds, L, M, Nu, rcn, xu, tol, maxit, &st, gis
+    const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
+    iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
 #ifdef MPCT_PROFILE
                          , pacc, pprev
 #endif
@@ -878,7 +687,8 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
 }
 
 // the instance launch_closed_loop picks (mpct_kernel_instance): QP size class, DTC, EXT
-std::string closed_loop_instance(int maxM, bool dtc, bool ext) {
+std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext) {
+  const bool dtc = sc.dtc != 0;
   const int cls = maxM <= 16 ? 16 : maxM <= 32 ? 32 : 64;
   return "gpc_closed_loop_kernel<" + std::to_string(cls) + (dtc ? ",true" : ",false") + (ext ? ",true>" : ",false>");
 }

@@ -1,0 +1,248 @@
+// gpc_qp.h — the per-step QP of the linear closed-loop kernel (gpc_closed_loop_kernel):
+// Goldfarb-Idnani on the box-constrained moves
+// (rate / amplitude rows of MV blocks), warm-started from the previous step's active set
+// (gi_core.h).  Runs on lanes 0..M-1 of the wave with wave-uniform control flow.
+#pragma once
+#include "gi_core.h"
+
+#ifndef MPCT_GI_B
+// explicit R_A^-1 (gi_core.h gi_bdot): parallel dot products instead of serial solves.  Off: on the
+// metric grid it saves 1.6-3 % at one workgroup per CU but its M^2 of LDS per simulation costs
+// two workgroups per CU, 14 % at 8192 candidates (profiles/r02f_quad_experiment.txt)
+#define MPCT_GI_B 0
+#endif
+
+#ifndef MPCT_GI_REBUILD
+#define MPCT_GI_REBUILD 8  // J (and R_A) rebuilt from R^-1 after this many x M rotations (DESIGN.md §5;
+                           // 8 M: 5 % faster than 4 M on the metric grid, same parity, tools/ab_variants.sh)
+#endif
+
+namespace mpct {
+
+// normal of constraint p = 4m + kind: rows j0..m of the MV block, sign
+__device__ __forceinline__ void gi_normal(int p, const RowCons& rc, int& j0, int& mp, double& sg) {
+  mp = p >> 2;
+  const int kind = p & 3;
+  j0 = kind < 2 ? mp : mp - __builtin_amdgcn_readlane(rc.l, mp);
+  sg = (kind & 1) ? -1.0 : 1.0;
+}
+
+// the LDS arrays of one simulation's QP (lanes 0..M-1 are its rows)
+struct QPBufs {
+  const double* rinv;  // R^-1 (row-major)
+  double *xc;          // in: -, out: the optimal moves (lanes < M)
+  double *jt, *dv, *ra, *sl;
+  double *b, *w;       // B = R_A^-1 and the warm start's w (MPCT_GI_B)
+};
+
+// the QP of one step: unconstrained minimiser xu (lanes < M), u(t-1) of the lane's MV up_row
+template <int MAXM>
+__device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCons& rc, double up_row,
+                     double xu, double tol, int maxit, int* st, GIState<MAXM>& S
+#ifdef MPCT_PROFILE
+                     , unsigned long long* pacc, unsigned long long& pprev
+#endif
+                     ) {
+  const int lane = threadIdx.x;
+  const bool row = lane < M;
+  const double* sRi = Q.rinv;
+  double* sxc = Q.xc;
+  double* sJT = Q.jt;
+  double* sd = Q.dv;
+  double* sRA = Q.ra;
+  double* ssl = Q.sl;
+  double* sB = MPCT_GI_B ? Q.b : nullptr;
+  double* sw = Q.w;
+  if (!row) up_row = 0.0;
+  const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
+  auto slacks = [&](double x, double s[4]) {
+    const double pre = block_prefix<MAXM>(x, rc.l, Nu, row, sxc);
+    if (rc.l == 0) {
+      s[0] = x - lo_box;
+      s[1] = hi_box - x;
+      s[2] = INFINITY;
+      s[3] = INFINITY;
+    } else {
+      s[0] = x - rc.dmin;
+      s[1] = rc.dmax - x;
+      s[2] = pre - (rc.umin - up_row);
+      s[3] = (rc.umax - up_row) - pre;
+    }
+    if (!row) s[0] = s[1] = s[2] = s[3] = INFINITY;
+  };
+  int it = 0;
+  double xm = xu;
+  {
+    // the unconstrained minimiser is optimal when it is feasible (the retained set is kept)
+    double s[4];
+    slacks(xu, s);
+    const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
+    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
+    if (S.q == 0) {
+      S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
+    } else {
+      if (row) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
+      }
+      if (!S.jinit || S.nrot >= MPCT_GI_REBUILD * M) {
+        // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
+        const int qq = S.q;
+        gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
+        S.q = 0;
+        for (int v = 0; v < qq; ++v) {
+          const int p = __builtin_amdgcn_readlane(S.ww, v);
+          int j0, mp;
+          double sg;
+          gi_normal(p, rc, j0, mp, sg);
+          const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sg, row);
+          const double beta = qsum<MAXM>(lane >= v ? dk * dk : 0.0);
+          lds_sync();
+          const double zm = gi_z(sJT, sd, v, M, row);
+          const double rv = MPCT_GI_B ? gi_bdot(sB, sd, v, M) : 0.0;
+          const double uk = S.uw;
+          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row, BoxMark{}, sB, rv);
+          if (lane == v) S.uw = uk;
+          ++it;
+        }
+        S.nrot = 0;
+      }
+      lds_sync();
+      // equality-constrained solve on the retained set, dropping negative multipliers
+      for (;;) {
+        const int q = S.q;
+        if (q == 0) {
+          xm = xu;
+          break;
+        }
+        double c = 0.0;
+        if (lane < q) c = -ssl[S.ww];  // b_A - N_A'x_u
+        double lam;
+        xm = xu;
+        if constexpr (MPCT_GI_B) {  // w = B'c, x = x_u + J(:,0:q) w, lambda = B w
+          if (lane < q) sd[lane] = c;
+          lds_sync();
+          const double wk = gi_btdot(sB, sd, q, M);
+          if (lane < q) sw[lane] = wk;
+          lds_sync();
+          if (row) {
+            double x1 = 0.0;
+            int v = 0;
+            for (; v + 1 < q; v += 2) {
+              xm += sJT[v * M + lane] * sw[v];
+              x1 += sJT[(v + 1) * M + lane] * sw[v + 1];
+            }
+            if (v < q) xm += sJT[v * M + lane] * sw[v];
+            xm += x1;
+          }
+          lam = gi_bdot(sB, sw, q, M);
+        } else {
+          double wv = 0.0;
+          for (int v = 0; v < q; ++v) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
+            const double w = bcast(c * S.rdg, v);
+            if (lane == v) wv = w;
+            if (lane > v && lane < q) c -= sRA[v * M + lane] * w;
+            if (row) xm += sJT[v * M + lane] * w;
+          }
+          lam = gi_backsub<MAXM>(S, sRA, M, wv);
+        }
+        if (lane < q) S.uw = lam;
+        double lmin = lane < q ? lam : INFINITY;
+        int kd = lane;
+        qargmin<MAXM>(lmin, kd);
+        if (!(lmin < 0.0)) break;
+        gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{}, sB);
+        ++it;
+      }
+      if (!row) xm = 0.0;
+    }
+  }
+  PSTAMP(PROF_QWARM);
+#ifdef MPCT_DEBUG_SIM
+  if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0) printf("QP entry-after-warm q=%d it=%d nrot=%d\n", S.q, it, S.nrot);
+#endif
+  for (;;) {
+    // ---- most violated inactive constraint
+    double best = INFINITY;
+    int bid = 0x7fffffff;
+    {
+      double s[4];
+      slacks(xm, s);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (!((S.act >> k) & 1u) && s[k] < best) {
+          best = s[k];
+          bid = 4 * lane + k;
+        }
+    }
+    qargmin<MAXM>(best, bid);
+    PSTAMP(PROF_QCHECK);
+    if (!(best < -tol)) break;
+    if (it >= maxit || S.q >= M) {
+      *st |= MPCT_ST_QP_MAXITER_;
+      break;
+    }
+    if (!S.jinit) gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
+    const int p = bid;
+    int j0, mp;
+    double sgp;
+    gi_normal(p, rc, j0, mp, sgp);
+    double sp = best;  // slack of p along the path
+    double upm = 0.0;  // its multiplier
+    bool infeas = false;
+    for (;;) {
+      ++it;
+      const double dk = gi_dvec<MAXM>(sJT, sd, M, j0, mp, sgp, row);
+      const double d2 = dk * dk;
+      const double dn2 = qsum<MAXM>(d2);
+      const double beta = qsum<MAXM>(lane >= S.q ? d2 : 0.0);
+      lds_sync();
+      const double zm = gi_z(sJT, sd, S.q, M, row);
+      PSTAMP(PROF_QD);
+      const double rk = MPCT_GI_B ? gi_bdot(sB, sd, S.q, M) : gi_backsub<MAXM>(S, sRA, M, dk);
+      // dual step over active constraints with r_w > 0
+      double t1 = INFINITY;
+      int kdrop = 0x7fffffff;
+      if (lane < S.q && rk > 0.0) {
+        t1 = S.uw / rk;
+        kdrop = lane;
+      }
+      qargmin<MAXM>(t1, kdrop);
+      PSTAMP(PROF_QR);
+      const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
+      if (t1 == INFINITY && t2 == INFINITY) {
+        *st |= MPCT_ST_QP_INFEAS_;
+        infeas = true;
+        break;
+      }
+      const bool full = t2 <= t1;
+      const double t = full ? t2 : t1;
+#ifdef MPCT_DEBUG_SIM
+      if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0 && it > 40 && it < 70)
+        printf("it=%d q=%d p=%d sp=%.3e beta=%.3e dn2=%.3e t1=%.3e t2=%.3e kd=%d %s\n", it, S.q, p, sp, beta, dn2, t1, t2, kdrop, full ? "ADD" : "DROP");
+#endif
+      if (t2 != INFINITY) xm += t * zm;
+      if (lane < S.q) S.uw -= t * rk;
+      upm += t;
+      sp += t * beta;
+      if (full) {
+        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{}, sB, rk);
+        PSTAMP(PROF_QADD);
+        break;
+      }
+      gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{}, sB);
+      PSTAMP(PROF_QDROP);
+      if (it >= maxit) {
+        *st |= MPCT_ST_QP_MAXITER_;
+        break;
+      }
+    }
+    if (it >= maxit || infeas) break;
+  }
+  if (row) sxc[lane] = xm;
+  lds_sync();
+  return it;
+}
+
+
+}  // namespace mpct

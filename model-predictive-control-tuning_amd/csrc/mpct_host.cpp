@@ -30,7 +30,7 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
                        WorkOrder* wo, hipStream_t stream, std::string* err);
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
-std::string closed_loop_instance(int maxM, bool dtc, bool ext);
+std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext);
 // defined in mdband_kernel.hip
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                   const double* lambda, const double* r, const double* v, const DevOpts& o, const DevResult& out,
@@ -1139,8 +1139,17 @@ extern "C" int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts*
     nm = "nmpc_closed_loop_kernel (QP-size x LDS-tier class launches)";
   else if (s->mdband)
     nm = "mdband_closed_loop_kernel (QP-size x LDS-tier class launches)";
-  else
-    nm = closed_loop_instance(s->nu * s->numax, s->dtc != 0, ext);
+  else {
+    DevScenario ds{};  // the fields the kernel choice reads
+    ds.my = s->my;
+    ds.nu = s->nu;
+    ds.nd = s->nd + s->nq;
+    ds.nin = s->npin;
+    ds.nx = s->nx;
+    ds.dtc = s->dtc;
+    ds.regpath = regpath(s);
+    nm = closed_loop_instance(ds, s->nu * s->numax, ext);
+  }
   if (buf && cap > 0) {
     const size_t n = std::min<size_t>(nm.size(), (size_t)cap - 1);
     std::memcpy(buf, nm.data(), n);
