@@ -18,7 +18,9 @@
 //     residual column): no Jacobian is stored, and the QP never sees normal equations (the rate
 //     weights span 1e-11..1 against the output rows' 1e2: cond(H) ~ 1e15, cond(R) ~ 3e7);
 //   * the step solves the box QP with the Goldfarb-Idnani dual method of gi_core.h (J = R^-1);
-//   * v += step; stop when the largest absolute-move change / s_u <= sqp_tol (the oracle's test).
+//   * v += step (Armijo backtracking), or the Anderson-accelerated point (depth 1: a secant on the
+//     last two Gauss-Newton points) when it meets the same decrease; stop when the largest
+//     absolute-move change of the full step / s_u <= sqp_tol (the oracle's test).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -277,6 +279,42 @@ __global__ void __launch_bounds__(64, 1)
   // (this lane's increment), state x, last move ul[n], reference (r0, r1).  Returns v.
   auto controller = [&](const double x[3], const double ul[2], double r0, double r1, double v)
                         __attribute__((always_inline)) -> double {
+    const double ulb = bn == 0 ? ul[0] : ul[1];
+    // cost f(v') of increments v' by a tangent-free forward pass; xin: every predicted state
+    // inside the hard state bounds
+    auto trial = [&](double va, bool& xin) __attribute__((always_inline)) -> double {
+      lds_sync();
+      if (row) sxc[lane] = va;
+      lds_sync();
+      if (row) {
+        double cum = 0.0;
+        for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
+        sU[lane] = ulb + cum;
+      }
+      lds_sync();
+      double xa[3] = {x[0], x[1], x[2]};
+      double fa = 0.0;
+      bool inb = true;
+      for (int i = 0; i < N; ++i) {
+        const int li = i < Nu - 1 ? i : Nu - 1;
+        const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
+        vdv_rk4<false>(P, h, nsub, xa, u, nullptr, nullptr);
+        const double e0 = wy0 * (sel3(xa, xc0) - r0);
+        fa += e0 * e0;
+        if (ny > 1) {
+          const double e1 = wy1 * (sel3(xa, xc1) - r1);
+          fa += e1 * e1;
+        }
+        if (has_xb)
+          for (int s = 0; s < 3; ++s) inb = inb && xa[s] >= txmin[s] && xa[s] <= txmax[s];
+      }
+      xin = inb;
+      return 0.5 * (fa + qsum<MAXM>(row ? (wu * va) * (wu * va) : 0.0));
+    };
+    // Anderson acceleration (depth 1) of the Gauss-Newton map v -> G(v) = v + d(v): the previous
+    // iteration's absolute-move step (aa_f, this lane's entry) and G (aa_g, increments)
+    bool aa_hist = false;
+    double aa_f = 0.0, aa_g = 0.0;
     for (int it = 0; it < sc.sqp_max; ++it) {
       ++sqp_total;
       // absolute moves of the iterate: U[n][l] = ul[n] + sum_{l' <= l} v[n][l']
@@ -477,41 +515,47 @@ __global__ void __launch_bounds__(64, 1)
         st |= MPCT_ST_NONFINITE_;
         return v;
       }
-      // ---- Armijo backtracking on the cost along the step (oracle/nmpc_vdv.py controller):
-      // dd = r'J s = c'R s, then halve alpha until f(v + alpha s) <= f0 + c1 alpha dd or the
-      // cost change is below its own rounding; the last alpha is taken regardless
+      // ---- directional derivative of the cost along the step: dd = r'J s = c'R s
       if (row) sxc[lane] = xm;
       lds_sync();
       double rs = 0.0;
       if (row)
         for (int j = lane; j < M; ++j) rs += sR[lane * M + j] * sxc[j];
       const double dd = qsum<MAXM>(row ? scv[lane] * rs : 0.0);
-      double alpha = 1.0;
-      for (int ls = 0; ls < kLsMax; ++ls) {
-        const double va = v + (row ? alpha * xm : 0.0);
-        lds_sync();
-        if (row) sxc[lane] = va;
-        lds_sync();
-        if (row) {
-          double cum = 0.0;
-          for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
-          sU[lane] = (bn == 0 ? ul[0] : ul[1]) + cum;
-        }
-        lds_sync();
-        double xa[3] = {x[0], x[1], x[2]};
-        double fa = 0.0;
-        for (int i = 0; i < N; ++i) {
-          const int li = i < Nu - 1 ? i : Nu - 1;
-          const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
-          vdv_rk4<false>(P, h, nsub, xa, u, nullptr, nullptr);
-          const double e0 = wy0 * (sel3(xa, xc0) - r0);
-          fa += e0 * e0;
-          if (ny > 1) {
-            const double e1 = wy1 * (sel3(xa, xc1) - r1);
-            fa += e1 * e1;
+      // ---- Anderson step (oracle/nmpc_vdv.py AA_DEPTH = 1): gamma = <df, d>/<df, df> on the
+      // absolute moves scaled by 1/s_u, candidate clip(G(v) - gamma (G(v) - G(v'))); taken when
+      // it meets the Armijo decrease of the full step and respects the state bounds
+      const double gv = v + (row ? xm : 0.0);
+      bool taken = false;
+      if (aa_hist) {
+        const double wdf = row ? (dpre - aa_f) / sun : 0.0;
+        const double den = qsum<MAXM>(wdf * wdf);
+        if (den > 0.0) {
+          const double gam = qsum<MAXM>(row ? wdf * (dpre / sun) : 0.0) / den;
+          const double vc0 = row ? gv - gam * (gv - aa_g) : 0.0;
+          const double pc = block_prefix<MAXM>(vc0, bl, Nu, row, sxc);
+          const double ucl = fmin(fmax(ulb + pc, lbn), ubn);
+          const double upl = lane_prev<MAXM>(ucl);
+          const double vc = row ? (bl == 0 ? ucl - ulb : ucl - upl) : 0.0;
+          bool xin;
+          const double fc = trial(vc, xin);
+          if (xin && fc <= f0 + kLsC1 * dd) {
+            v = vc;
+            taken = true;
           }
         }
-        const double f1 = 0.5 * (fa + qsum<MAXM>(row ? (wu * va) * (wu * va) : 0.0));
+      }
+      aa_f = row ? dpre : 0.0;
+      aa_g = gv;
+      aa_hist = true;
+      if (taken) continue;
+      // ---- Armijo backtracking on the cost along the step (oracle/nmpc_vdv.py controller):
+      // halve alpha until f(v + alpha s) <= f0 + c1 alpha dd or the cost change is below its own
+      // rounding; the last alpha is taken regardless
+      double alpha = 1.0;
+      for (int ls = 0; ls < kLsMax; ++ls) {
+        bool xin;
+        const double f1 = trial(v + (row ? alpha * xm : 0.0), xin);
         if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) break;
         alpha *= 0.5;
       }
