@@ -1,8 +1,18 @@
 #!/bin/bash
-# Build a libmpct variant with extra defines for the gpc kernel:  bash tools/variant.sh NAME -DFOO=1 ...
+# Build a libmpct variant with extra defines for one kernel unit (default gpc_kernel.hip; K=mdband_kernel.hip
+# or K=nmpc_kernel.hip for the others) and the host unit:  [K=unit.hip] bash tools/variant.sh NAME -DFOO=1 ...
 set -e
 C=/root/repo/model-predictive-control-tuning_amd/csrc; NAME=$1; shift
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c $C/gpc_kernel.hip -o /tmp/gpc_$NAME.o
+K=${K:-gpc_kernel.hip}
+OBJS=""
+for u in gpc_kernel mdband_kernel nmpc_kernel work_order; do
+  if [ "$u.hip" = "$K" ]; then
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c $C/$K -o /tmp/${u}_$NAME.o
+    OBJS="$OBJS /tmp/${u}_$NAME.o"
+  else
+    OBJS="$OBJS $C/$u.o"
+  fi
+done
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c $C/mpct_host.cpp -o /tmp/host_$NAME.o
-hipcc --offload-arch=gfx950 -shared -fPIC /tmp/gpc_$NAME.o $C/mdband_kernel.o $C/nmpc_kernel.o $C/work_order.o /tmp/host_$NAME.o -o $C/libmpct_$NAME.so
+hipcc --offload-arch=gfx950 -shared -fPIC $OBJS /tmp/host_$NAME.o -o $C/libmpct_$NAME.so
 echo built $C/libmpct_$NAME.so
