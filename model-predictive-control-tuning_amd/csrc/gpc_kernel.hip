@@ -106,7 +106,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
                            const double* __restrict__ deltav, const double* __restrict__ lambdav,
                            const double* __restrict__ rv, const double* __restrict__ vv,
-                           const int* __restrict__ perm, const DevOpts o, const DevResult out) {
+                           const int* __restrict__ perm, const DevOpts o, const DevResult out, int mlo,
+                           int first) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   // workgroup slot -> candidate: perm (heaviest estimated work first, see order_candidates) or
@@ -139,13 +140,14 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     }
   };
   if (N2 <= 0) {
-    write_nan(MPCT_ST_SKIPPED_);
+    if (first) write_nan(MPCT_ST_SKIPPED_);
     return;
   }
-  if (N2 > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N2 || M > MAXM) {
-    write_nan(MPCT_ST_BADHORIZON_);
+  if (N2 > sc.n2max || Nu < 1 || Nu > sc.numax || Nu > N2) {
+    if (first) write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
+  if (M <= mlo || M > MAXM) return;  // another QP-size class launch simulates it
   const LdsLayout L = lds_layout(sc, M);
   const int nxp = (nx + 1) & ~1;  // padded row length of A (x[nx] and the pad column are 0)
   double* sRi = lds + L.rinv;
@@ -641,6 +643,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
 #include <string>
 
 #include "work_order.h"
+#include "launch_fan.h"
 
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
@@ -655,12 +658,15 @@ long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {
   return (long long)L.total * 8;
 }
 
+// one QP-size class launch over the whole batch: simulations with mlo < M <= MAXM run here (first:
+// this launch also writes the statuses of skipped / bad-horizon candidates)
 template <int MAXM>
 static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                     const double* delta, const double* lambda, const double* r, const double* v,
-                    const DevOpts& o, const DevResult& out, const int* perm, hipStream_t stream,
-                    std::string* err) {
-  const long long lds = lds_bytes_for(sc, sc.n2max, sc.numax);
+                    const DevOpts& o, const DevResult& out, const int* perm, int mlo, int first,
+                    hipStream_t stream, std::string* err) {
+  const int nu_cls = sc.numax < MAXM / sc.nu ? sc.numax : MAXM / sc.nu;  // largest Nu of this class
+  const long long lds = lds_bytes_for(sc, sc.n2max, nu_cls);
   if (lds > 160 * 1024) {
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
@@ -677,7 +683,7 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
   }
   const long long S = C * nref;
   hipLaunchKernelGGL(kern, dim3((unsigned)S), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
-                     delta, lambda, r, v, perm, o, out);
+                     delta, lambda, r, v, perm, o, out, mlo, first);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
@@ -686,17 +692,26 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
   return 0;
 }
 
-// the instance launch_closed_loop picks (mpct_kernel_instance): QP size class, DTC, EXT
+// QP-size classes a scenario launches: <16> for M <= 16, then <32>, <64> up to nu * nu_max (a
+// batch with mixed Nu runs each simulation in the smallest class that holds it: the <16> instance
+// has DPP reductions over one row and three waves per SIMD)
+static int top_class(int maxM) { return maxM <= 16 ? 16 : maxM <= 32 ? 32 : 64; }
+
+// the instance(s) launch_closed_loop picks (mpct_kernel_instance): QP size classes, DTC, EXT
 std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext) {
-  const bool dtc = sc.dtc != 0;
-  const int cls = maxM <= 16 ? 16 : maxM <= 32 ? 32 : 64;
-  return "gpc_closed_loop_kernel<" + std::to_string(cls) + (dtc ? ",true" : ",false") + (ext ? ",true>" : ",false>");
+  const std::string tail = std::string(sc.dtc ? ",true" : ",false") + (ext ? ",true>" : ",false>");
+  std::string nm;
+  for (int cls = 16; cls <= top_class(maxM); cls *= 2) {
+    if (sc.nu > cls) continue;
+    nm += (nm.empty() ? "gpc_closed_loop_kernel<" : " + <") + std::to_string(cls) + tail;
+  }
+  return nm;
 }
 
 int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                        const double* delta, const double* lambda, const double* r,
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
-                       WorkOrder* wo, hipStream_t stream, std::string* err) {
+                       WorkOrder* wo, LaunchFan* fan, hipStream_t stream, std::string* err) {
   if (maxM > 64) {
     *err = "nu*nu_max > 64";
     return -4;
@@ -706,10 +721,23 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const int rc = order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err);
     if (rc) return rc;
   }
-  int rc;
-  if (maxM <= 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
-  else if (maxM <= 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
-  else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, stream, err);
+  int rc = 0;
+  FanScope fs(top_class(maxM) > 16 ? fan : nullptr, stream);
+  int k = 0, mlo = 0;
+  for (int cls = 16; cls <= top_class(maxM) && rc == 0; cls *= 2) {
+    if (sc.nu > cls) {  // no simulation fits this class
+      mlo = cls;
+      continue;
+    }
+    const hipStream_t st = fs.stream(k);
+    const int first = k == 0;
+    if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
+    else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
+    else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
+    mlo = cls;
+    ++k;
+  }
+  fs.join();
   if (perm) order_mark_used(*wo, stream);
   return rc;
 }

@@ -28,7 +28,7 @@ namespace mpct {
 int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu,
                        const double* delta, const double* lambda, const double* r,
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
-                       WorkOrder* wo, hipStream_t stream, std::string* err);
+                       WorkOrder* wo, LaunchFan* fan, hipStream_t stream, std::string* err);
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
 std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext);
 // defined in mdband_kernel.hip
@@ -875,7 +875,7 @@ static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out) {
   ds.nm = reinterpret_cast<const double*>(b + o_nm);
   cx->dtab = dp;
   cx->dev = dev;
-  if ((s->mdband || s->nmpc) && !cx->fan.init(dev)) cx->fan.release();  // no fan: one stream, still correct
+  if (!cx->fan.init(dev)) cx->fan.release();  // class launches over streams; no fan: one stream, still correct
   s->ctx[dev] = cx;
   *out = cx;
   return MPCT_OK;
@@ -922,7 +922,7 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
   else if (s->mdband)
     rc = launch_mdband(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, stream, &cx->fan, &err);
   else
-    rc = launch_closed_loop(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &cx->order,
+    rc = launch_closed_loop(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &cx->order, &cx->fan,
                             stream, &err);
   if (rc) return fail(rc, err);
 #ifdef MPCT_PROFILE

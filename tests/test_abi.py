@@ -258,9 +258,11 @@ def test_kernel_instance_and_multi_validation(built):
     assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,false,false>"
     assert kernel_instance(sc, open_loop=True) == "gpc_closed_loop_kernel<16,false,true>"
     sc6, _, _ = shell3x3(n2_max=30, nu_max=6)
-    assert kernel_instance(sc6) == "gpc_closed_loop_kernel<32,false,false>"
+    # mixed Nu: every simulation runs in the smallest QP-size class that holds it
+    assert kernel_instance(sc6) == "gpc_closed_loop_kernel<16,false,false> + <32,false,false>"
     sc15, _, _ = shell3x3(n2_max=127, nu_max=15)
-    assert kernel_instance(sc15, want_traj=True) == "gpc_closed_loop_kernel<64,false,true>"
+    assert kernel_instance(sc15, want_traj=True) == ("gpc_closed_loop_kernel<16,false,true> + <32,false,true> + "
+                                                     "<64,false,true>")
     N2 = np.full(4, 30, np.int32)
     d = np.full((4, 3), 0.1)
     with pytest.raises(MpctError, match="duplicate"):

@@ -178,8 +178,8 @@ def test_config4_range_against_oracle(gpu):
     assert len(np.unique(Nu)) >= 2 and Nu.max() * 2 > 16
     from mpct.engine import kernel_instance
 
-    assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<32,true,true>"
-    assert kernel_instance(sc) == "gpc_closed_loop_kernel<32,true,false>"
+    assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<16,true,true> + <32,true,true>"
+    assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,true,false> + <32,true,false>"
     res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
     cost = eval_batch(sc, N2, Nu, d, l, refs, v=v)   # the cost-only instance the bench times
     ok = res.status == 0
