@@ -315,19 +315,23 @@ __global__ void __launch_bounds__(64, 1)
     // iteration's absolute-move step (aa_f, this lane's entry) and G (aa_g, increments)
     bool aa_hist = false;
     double aa_f = 0.0, aa_g = 0.0;
-    for (int it = 0; it < sc.sqp_max; ++it) {
-      ++sqp_total;
+    // the prediction at increments va with its forward tangents, streamed into the Givens QR of the
+    // least-squares Jacobian [rate rows; output rows] (R and c = Q'r -> LDS), the state rows of the
+    // linearised bounds (LDS) and the cost f(va); xin: every predicted state inside the hard bounds.
+    // Also the trial pass of a step: when the step is taken, its factorisation is the next
+    // iteration's, so an accepted trial costs one prediction instead of two.
+    auto full_pass = [&](double va, bool& xin) __attribute__((always_inline)) -> double {
       // absolute moves of the iterate: U[n][l] = ul[n] + sum_{l' <= l} v[n][l']
-      if (row) sxc[lane] = v;
+      lds_sync();
+      if (row) sxc[lane] = va;
       lds_sync();
       double cum = 0.0;
       if (row) {
         for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
         sU[lane] = (bn == 0 ? ul[0] : ul[1]) + cum;
-        srw[lane] = wu * v;
+        srw[lane] = wu * va;
       }
       lds_sync();
-      // ---- least-squares Jacobian [rate rows; output rows] by row-streamed Givens QR
       double rcol[MAXM];
 #pragma unroll
       for (int k = 0; k < MAXM; ++k) {
@@ -341,6 +345,7 @@ __global__ void __launch_bounds__(64, 1)
       double xs[3] = {x[0], x[1], x[2]};
       double td[3] = {0.0, 0.0, 0.0};
       double fo = 0.0;  // sum of squared output residuals (lane M)
+      bool inb = true;
       for (int i = 0; i < N; ++i) {
         const int li = i < Nu - 1 ? i : Nu - 1;
         const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
@@ -357,6 +362,7 @@ __global__ void __launch_bounds__(64, 1)
             sxp[i * 3 + 1] = xs[1];
             sxp[i * 3 + 2] = xs[2];
           }
+          for (int s3 = 0; s3 < 3; ++s3) inb = inb && xs[s3] >= txmin[s3] && xs[s3] <= txmax[s3];
         }
         for (int j = 0; j < ny; ++j) {
           const int xj = j == 0 ? xc0 : xc1;
@@ -390,7 +396,19 @@ __global__ void __launch_bounds__(64, 1)
             else scv[k] = rcol[k];
           }
       }
-      const double f0 = 0.5 * (bcast(fo, M) + qsum<MAXM>(row ? (wu * v) * (wu * v) : 0.0));
+      xin = inb;
+      return 0.5 * (bcast(fo, M) + qsum<MAXM>(row ? (wu * va) * (wu * va) : 0.0));
+    };
+    bool have = false;  // LDS holds the factorisation at v (an accepted trial pass)
+    double fcur = 0.0;
+    for (int it = 0; it < sc.sqp_max; ++it) {
+      ++sqp_total;
+      if (!have) {
+        bool xin_;
+        fcur = full_pass(v, xin_);
+      }
+      have = false;
+      const double f0 = fcur;
       lds_sync();
       // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
       if (row) {
@@ -538,10 +556,12 @@ __global__ void __launch_bounds__(64, 1)
           const double upl = lane_prev<MAXM>(ucl);
           const double vc = row ? (bl == 0 ? ucl - ulb : ucl - upl) : 0.0;
           bool xin;
-          const double fc = trial(vc, xin);
+          const double fc = full_pass(vc, xin);
           if (xin && fc <= f0 + kLsC1 * dd) {
             v = vc;
             taken = true;
+            have = true;
+            fcur = fc;
           }
         }
       }
@@ -555,8 +575,16 @@ __global__ void __launch_bounds__(64, 1)
       double alpha = 1.0;
       for (int ls = 0; ls < kLsMax; ++ls) {
         bool xin;
-        const double f1 = trial(v + (row ? alpha * xm : 0.0), xin);
-        if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) break;
+        // the full step's trial is a full pass (usually taken), shorter steps a tangent-free one
+        const double va = v + (row ? alpha * xm : 0.0);
+        const double f1 = ls == 0 ? full_pass(va, xin) : trial(va, xin);
+        if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
+          if (ls == 0) {
+            have = true;
+            fcur = f1;
+          }
+          break;
+        }
         alpha *= 0.5;
       }
       v += row ? alpha * xm : 0.0;
