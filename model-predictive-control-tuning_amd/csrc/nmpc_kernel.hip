@@ -377,9 +377,14 @@ __global__ void __launch_bounds__(64, 1)
             if (k < M) {
               const double b = bcast(w, k);
               const double a = bcast(rcol[k], k);
-              const double rho = sqrt(a * a + b * b);
+              // 1/rho by v_rsq_f64 and two Newton steps (a divide-free chain, as gpc_kernel's QR)
+              const double xx = a * a + b * b;
+              double ri = __builtin_amdgcn_rsq(xx);
+              const double hx = 0.5 * xx;
+              ri = ri * fma(-hx * ri, ri, 1.5);
+              ri = ri * fma(-hx * ri, ri, 1.5);
               const bool nz = b != 0.0;
-              const double cs = nz ? a / rho : 1.0, sn = nz ? b / rho : 0.0;
+              const double cs = nz ? a * ri : 1.0, sn = nz ? b * ri : 0.0;
               const double rk = rcol[k];
               rcol[k] = cs * rk + sn * w;
               w = -sn * rk + cs * w;
