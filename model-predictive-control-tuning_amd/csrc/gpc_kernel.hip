@@ -472,7 +472,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    if (ln < ncopy * ne) {
+#ifndef MPCT_EXP_SKIP
+#define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
+#endif
+    if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double acc;
@@ -517,7 +520,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
       }
       lds_sync();
     }
-    if (ln < my) {
+    if (!(MPCT_EXP_SKIP & 2) && ln < my) {
       const int i = lane;
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
@@ -583,8 +586,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
     }
     lds_sync();
     PSTAMP(PROF_YUPD);
-    solve_step();
-    if (ln < nu) {
+    if (!(MPCT_EXP_SKIP & 4)) solve_step();
+    if (!(MPCT_EXP_SKIP & 8) && ln < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
