@@ -29,6 +29,9 @@
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
                              // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
 #endif
+#ifndef MPCT_WAVES32
+#define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
+#endif
 #ifndef MPCT_REG_DU
 #define MPCT_REG_DU 0  // past-control registers in VGPRs (else shifted in LDS; 0 measured faster)
 #endif
@@ -101,7 +104,7 @@ __device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m
 // EXT: the open-loop prediction and/or trajectories may be requested; the EXT = false instance
 // (GAM scoring: costs only) carries none of their state through the step loop
 template <int MAXM, bool DTC, bool EXT>
-__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : 1)
+__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 32 ? MPCT_WAVES32 : 1))
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
                            const double* __restrict__ deltav, const double* __restrict__ lambdav,
