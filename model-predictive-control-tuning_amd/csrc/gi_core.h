@@ -4,7 +4,14 @@
 #pragma once
 #include "wave_ops.h"
 
+#ifndef MPCT_QP_FASTDIV
+#define MPCT_QP_FASTDIV 1  // QP step lengths, Householder / Givens scalars by rcp_nr / rsq_nr (0: IEEE / and sqrt)
+#endif
+
 namespace mpct {
+
+__device__ __forceinline__ double qp_div(double a, double b) { return MPCT_QP_FASTDIV ? a * rcp_nr(b) : a / b; }
+__device__ __forceinline__ double qp_rcp(double b) { return MPCT_QP_FASTDIV ? rcp_nr(b) : 1.0 / b; }
 
 // constraint p = 4*m + kind on move m = n*Nu + l:
 //   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
@@ -167,10 +174,10 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
   const int lane = threadIdx.x;
   const int q = S.q;
   const double dq = bcast(dk, q);
-  const double nrm = sqrt(beta);
+  const double nrm = MPCT_QP_FASTDIV ? beta * rsq_nr(beta) : sqrt(beta);  // beta > 0 on an add
   const double alpha = dq > 0.0 ? -nrm : nrm;
   const double vq = dq - alpha;
-  const double two_vtv = 1.0 / (beta - alpha * dq);  // 2 / v'v
+  const double two_vtv = qp_rcp(beta - alpha * dq);  // 2 / v'v
   if (row) {
     const double jq = sJT[q * M + lane];
     const double f = (zm - alpha * jq) * two_vtv;
@@ -178,7 +185,7 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
   if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
-  const double ia = 1.0 / alpha;
+  const double ia = qp_rcp(alpha);
   if (lane == q) {
     sRA[q * M + q] = alpha;
     S.rdg = ia;
@@ -222,9 +229,9 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
   for (int jj = kd; jj < q - 1; ++jj) {
     {
       const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
-      const double rho = sqrt(a * a + b * b);
-      if (rho != 0.0) {
-        const double ri = 1.0 / rho;
+      const double rr = a * a + b * b;
+      if (rr != 0.0) {
+        const double ri = MPCT_QP_FASTDIV ? rsq_nr(rr) : 1.0 / sqrt(rr);
         const double cs = a * ri, sn = b * ri;
         if (lane >= jj && lane < q - 1) {
           const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
@@ -254,7 +261,7 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
     S.uw = 0.0;
     S.ww = -1;
   }
-  if (lane < qn) S.rdg = 1.0 / sRA[lane * M + lane];
+  if (lane < qn) S.rdg = qp_rcp(sRA[lane * M + lane]);
   S.q = qn;
   lds_sync();
 }

@@ -204,12 +204,12 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
       if (lane < S.q && rk > 0.0) {
-        t1 = S.uw / rk;
+        t1 = qp_div(S.uw, rk);
         kdrop = lane;
       }
       qargmin<MAXM>(t1, kdrop);
       PSTAMP(PROF_QR);
-      const double t2 = (beta > 1e-14 * dn2) ? -sp / beta : INFINITY;
+      const double t2 = (beta > 1e-14 * dn2) ? -qp_div(sp, beta) : INFINITY;
       if (t1 == INFINITY && t2 == INFINITY) {
         *st |= MPCT_ST_QP_INFEAS_;
         infeas = true;

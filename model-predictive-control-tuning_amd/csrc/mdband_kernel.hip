@@ -587,11 +587,11 @@ __global__ void __launch_bounds__(64, 1)
         double t1 = INFINITY;
         int kdrop = 0x7fffffff;
         if (lane < gis.q && rk > 0.0) {
-          t1 = gis.uw / rk;
+          t1 = qp_div(gis.uw, rk);
           kdrop = lane;
         }
         qargmin<MAXM>(t1, kdrop);
-        const double t2 = (beta > 1e-20 * dn2) ? -sp / beta : INFINITY;
+        const double t2 = (beta > 1e-20 * dn2) ? -qp_div(sp, beta) : INFINITY;
         if (t1 == INFINITY && t2 == INFINITY) {
           st |= MPCT_ST_QP_INFEAS_;
           infeas = true;

@@ -53,18 +53,60 @@ __device__ __forceinline__ VdV vdv_load(const double* p) {
   return P;
 }
 
+#ifndef MPCT_RHS_FAST
+#define MPCT_RHS_FAST 1  // 1: 1/th by v_rcp_f64 + Newton (config 5: 326 -> 293 ms); 2: also exp by exp_estrin
+                         // (306 ms: more VALU than the libm exp, 2 % lower small-batch latency); 0: libm
+#endif
+
+// exp(x): Cody-Waite reduction by ln 2 (hi part with 32 trailing zero bits, so n*ln2_hi is exact),
+// degree-13 Taylor polynomial on |r| <= ln2/2 (truncation < 5e-18) by Estrin's scheme (dependency
+// depth 4 instead of Horner's 13), then 2^n by v_ldexp_f64.  Within 2 ulp of the correctly
+// rounded value; overflow -> inf and underflow -> 0 through ldexp.
+__device__ __forceinline__ double exp_estrin(double x) {
+  const double n = __builtin_rint(x * 1.4426950408889634074);
+  const double r = fma(-n, 1.90821492927058770002e-10, fma(-n, 6.93147180369123816490e-01, x));
+  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+  const double q0 = fma(r, 1.0, 1.0);
+  const double q1 = fma(r, 1.0 / 6.0, 0.5);
+  const double q2 = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  const double q3 = fma(r, 1.0 / 5040.0, 1.0 / 720.0);
+  const double q4 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0);
+  const double q5 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0);
+  const double q6 = fma(r, 1.0 / 6227020800.0, 1.0 / 479001600.0);
+  const double s0 = fma(q1, r2, q0), s1 = fma(q3, r2, q2), s2 = fma(q5, r2, q4);
+  const double t0 = fma(s1, r4, s0), t1 = fma(q6, r4, s2);
+  return __builtin_ldexp(fma(t1, r8, t0), (int)n);
+}
+
 // state derivative f(x, u) (nmpc_vandevusse_state.m:64-82) and, with TAN, its directional
 // derivative along (xd, ud)
 template <bool TAN>
 __device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const double u[2], const double xd[3],
                                         const double ud[2], double f[3], double fd[3]) {
   const double ca = x[0], cb = x[1], T = x[2];
+#if MPCT_EXP_RHS == 1  // ablation: one more exp in series on the rhs chain (value unchanged)
+  const double th = T + 273.15 + 0.0 * exp(T * 1e-3);
+#elif MPCT_EXP_RHS == 2  // ablation: one more division in series (value unchanged)
+  const double th = T + 273.15 + 0.0 * (1.0 / T);
+#else
   const double th = T + 273.15;
+#endif
+#if MPCT_RHS_FAST >= 1
+  const double ith = rcp_nr(th);
+#else
   const double ith = 1.0 / th;
+#endif
+#if MPCT_RHS_FAST >= 2
+  const double ex1 = exp_estrin(P.e1 * ith);
+  const double k1 = P.k10 * ex1;
+  const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp_estrin(P.e2 * ith));  // E1 = E2 in the reference model
+  const double k3 = P.k30 * exp_estrin(P.e3 * ith);
+#else
   const double ex1 = exp(P.e1 * ith);
   const double k1 = P.k10 * ex1;
   const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp(P.e2 * ith));  // E1 = E2 in the reference model
   const double k3 = P.k30 * exp(P.e3 * ith);
+#endif
   const double fov = u[0], tk = u[1];
   f[0] = fov * (P.ca0 - ca) - k1 * ca - k3 * ca * ca;
   f[1] = -fov * cb + k1 * ca - k2 * cb;
@@ -498,11 +540,11 @@ __global__ void __launch_bounds__(64, 1)
           double t1 = INFINITY;
           int kdrop = 0x7fffffff;
           if (lane < gis.q && rk > 0.0) {
-            t1 = gis.uw / rk;
+            t1 = qp_div(gis.uw, rk);
             kdrop = lane;
           }
           qargmin<MAXM>(t1, kdrop);
-          const double t2 = (beta > 1e-20 * dn2) ? -sp / beta : INFINITY;
+          const double t2 = (beta > 1e-20 * dn2) ? -qp_div(sp, beta) : INFINITY;
           if (t1 == INFINITY && t2 == INFINITY) {
             st |= MPCT_ST_QP_INFEAS_;
             infeas = true;

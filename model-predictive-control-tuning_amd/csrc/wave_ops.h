@@ -21,6 +21,22 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 1/x: v_rcp_f64 and two Newton steps (about 1 ulp, not correctly rounded): five dependent
+// operations instead of the division's scale / rcp / refine / fixup sequence
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// 1/sqrt(x), x > 0: v_rsq_f64 and two Newton steps (the Givens rotations' divide-free form)
+__device__ __forceinline__ double rsq_nr(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  r = r * fma(-h * r, r, 1.5);
+  return r * fma(-h * r, r, 1.5);
+}
+
 __device__ __forceinline__ double bcast(double v, int src) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
