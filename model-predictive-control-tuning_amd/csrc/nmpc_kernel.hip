@@ -207,8 +207,15 @@ struct StateMark {
   }
 };
 
+#ifndef MPCT_NMPC_WAVES16
+#define MPCT_NMPC_WAVES16 1  // VGPR budget of the M <= 16 class, in waves per SIMD: 2 or 3 spill and ran config 5
+#endif                       // 27 % slower (1 wave: 342 VGPRs; profiles/r02i_nmpc_code_size.txt)
+#ifndef MPCT_NMPC_WAVES32
+#define MPCT_NMPC_WAVES32 1
+#endif
+
 template <int MAXM>
-__global__ void __launch_bounds__(64, 1)
+__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 32 ? MPCT_NMPC_WAVES32 : 1))
     nmpc_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ Nv,
                             const int* __restrict__ Nuv, const double* __restrict__ deltav,
                             const double* __restrict__ lambdav, const double* __restrict__ rv,
