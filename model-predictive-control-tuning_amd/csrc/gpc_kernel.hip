@@ -724,7 +724,8 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
   }
   const int* perm = nullptr;
   if (wo) {
-    const int rc = order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err);
+    const int rc =
+        order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err, &sc, nref, r);
     if (rc) return rc;
   }
   int rc = 0;

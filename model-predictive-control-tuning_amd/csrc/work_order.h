@@ -15,13 +15,20 @@
 namespace mpct {
 
 enum OrderKind {
-  kOrderGpc = 0,   // GPC / DTC-GPC: QP size M, then the tracking-to-move weight ratio (more QP work)
+  kOrderGpc = 0,   // GPC / DTC-GPC: QP size M, then the unconstrained move demand (or the weight ratio)
   kOrderNmpc = 1,  // NMPC: horizon N and the weight ratio (fewer Gauss-Newton iterations)
 };
 
-// perm = nullptr when the batch is too small for the order to matter (kOrderMinC)
+// per-candidate work bound of the controller-based GPC key (multiply-adds for H); above it the
+// weight-ratio key is used
+constexpr double kOrderEstMaxCost = 1 << 20;
+
+// perm = nullptr when the batch is too small for the order to matter (kOrderMinC).  kOrderGpc with
+// the scenario and its reference signals (sc, nref, r: device [nref][my][nit]) keys on the
+// candidate's unconstrained move demand (order_keys_gpc); without them, on the weight ratio.
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
-                     const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err);
+                     const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
+                     const DevScenario* sc = nullptr, int nref = 0, const double* r = nullptr);
 
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);

@@ -1,6 +1,7 @@
 // work_order.hip — heaviest-first dispatch order of a candidate batch (see work_order.h).
 #include <hipcub/hipcub.hpp>
 
+#include "wave_ops.h"
 #include "work_order.h"
 
 namespace mpct {
@@ -12,7 +13,9 @@ namespace mpct {
 // weights predict: the more the tracking weights dominate the move-rate weights, the more often
 // the bounds bind.  Key (ascending = heavier first): ~(M << 20 | q(mean_j log2(max_i|delta_i| /
 // |lambda_j|))); invalid candidates last.  Measured on the metric batch (tools/order_probe.py):
-// grid order 5.36 ms, this key 3.9 ms, ideal (measured QP work, descending) 3.58 ms.
+// grid order 5.36 ms, this key 3.9 ms, ideal (measured QP work, descending) 3.58 ms.  GPC and
+// DTC-GPC batches now use the controller-based estimate of order_keys_gpc below; this weight-ratio
+// key remains for NMPC and for scenarios whose H is too large to form per candidate.
 // NMPC (config 5, tools/order_probe5.py, tools/nmpc_key_ab.sh): the Gauss-Newton iteration count
 // falls as the weight ratio grows (Spearman -0.54) while the work per iteration grows with the
 // horizon N and the QP size; score log(N Nu) - 0.1 a.  Closed loop of the 4096 grid: grid order
@@ -47,9 +50,152 @@ __global__ void order_keys(int kind, long long C, int my, int nu, const int* __r
   idx[c] = (int)c;
 }
 
+// GPC / DTC-GPC key from the candidate's own controller: its unconstrained move demand for the
+// scenario's setpoint jumps, in units of each MV's bounds.  H = G'QG + Lambda with the weights as
+// the closed-loop kernel's QR applies them; w_i = H^-1 G'Q 1_i are the moves answering a unit
+// step held on output i over the horizon, so a reference jump d asks for z = sum_i d_i w_i.  The
+// more |z| exceeds the bounds, the more steps run active QP rows.  On the metric grid this
+// estimate ranks the measured QP work with Spearman 0.93 (the weight-ratio key above: 0.58), and
+// dispatching in its order takes 3.44 ms against the weight-ratio key's 3.90 ms and the measured-
+// work order's 3.48 ms (tools/diag/order_key_probe.py).  One wave per candidate: H by lanes
+// over its entries (step-table correlations), Cholesky and the my solves in LDS, lanes over the
+// reference's time steps for the jumps.
+__global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long long C, int nref,
+                                                      const int* __restrict__ N2v, const int* __restrict__ Nuv,
+                                                      const double* __restrict__ delta,
+                                                      const double* __restrict__ lambda,
+                                                      const double* __restrict__ r, unsigned* __restrict__ key,
+                                                      int* __restrict__ idx) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const long long c = blockIdx.x;
+  if (c >= C) return;
+  const int lane = threadIdx.x;
+  const int my = sc.my, nu = sc.nu, tlen = sc.tlen, nit = sc.nit;
+  const int n2 = N2v[c], nuc = Nuv[c];
+  if (lane == 0) idx[c] = (int)c;
+  if (!(n2 > 0 && n2 <= sc.n2max && nuc >= 1 && nuc <= sc.numax && nuc <= n2)) {
+    if (lane == 0) key[c] = 0xffffffffu;
+    return;
+  }
+  const int M = nu * nuc;
+  const int Mp = sc.nu * sc.numax;
+  double* sH = lds;             // H, then its Cholesky factor L (lower, row-major, stride M)
+  double* sW = lds + Mp * Mp;   // w_i (row i, stride M)
+  double* sQ = sW + my * Mp;    // q_i
+  if (lane < my) {
+    const double di = fabs(delta[c * my + lane]);
+    const double sqi = sc.wsq ? di : sqrt(di);
+    sQ[lane] = sqi * sqi;
+  }
+  lds_sync();
+  // H(a,b) = sum_i q_i sum_r G_i(r,a) G_i(r,b) + Lambda,  G_i(r, n*Nu + l) = s_in(n1_i + r - l)
+  for (int e = lane; e < M * M; e += kWave) {
+    const int a = e / M, b = e - a * M;
+    if (b < a) continue;
+    const int na = a / nuc, la = a - na * nuc, nb = b / nuc, lb = b - nb * nuc;
+    double h = 0.0;
+    for (int i = 0; i < my; ++i) {
+      const double* sa = sc.step + (long long)(i * nu + na) * tlen;
+      const double* sb = sc.step + (long long)(i * nu + nb) * tlen;
+      const int n1 = sc.n1[i];
+      const int r0 = la > lb ? la - n1 : lb - n1;  // first row where both indices are >= 0
+      double acc = 0.0;
+      for (int rr = r0 > 0 ? r0 : 0; rr < n2; ++rr) acc += sa[n1 + rr - la] * sb[n1 + rr - lb];
+      h += sQ[i] * acc;
+    }
+    if (a == b) {
+      const double ln = fabs(lambda[c * nu + na]);
+      const double wl = sc.wsq ? ln : sqrt(ln);
+      h += wl * wl;
+    }
+    sH[a * M + b] = h;
+    sH[b * M + a] = h;
+  }
+  // right-hand sides q_i G_i'1 (column sums of G_i)
+  for (int e = lane; e < my * M; e += kWave) {
+    const int i = e / M, m = e - i * M, n = m / nuc, l = m - n * nuc;
+    const double* si = sc.step + (long long)(i * nu + n) * tlen;
+    const int n1 = sc.n1[i];
+    double acc = 0.0;
+    for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) acc += si[n1 + rr - l];
+    sW[i * M + m] = sQ[i] * acc;
+  }
+  lds_sync();
+  // Cholesky H = L L' (lanes over the column below the pivot, then over the trailing block)
+  bool spd = true;
+  for (int k = 0; k < M; ++k) {
+    const double pk = sH[k * M + k];
+    if (!(pk > 0.0)) {
+      spd = false;
+      break;
+    }
+    const double lk = sqrt(pk), il = 1.0 / lk;
+    lds_sync();
+    for (int i = k + 1 + lane; i < M; i += kWave) sH[i * M + k] *= il;
+    if (lane == 0) sH[k * M + k] = lk;
+    lds_sync();
+    const int t = M - k - 1;
+    for (int e = lane; e < t * t; e += kWave) {
+      const int i = k + 1 + e / t, j = k + 1 + e % t;
+      if (j <= i) sH[i * M + j] -= sH[i * M + k] * sH[j * M + k];
+    }
+    lds_sync();
+  }
+  double est = INFINITY;  // a factorisation that fails: treat as heaviest
+  if (spd) {
+    // w_i = H^-1 rhs_i: lane i runs both triangular solves in place
+    if (lane < my) {
+      double* w = sW + lane * M;
+      for (int m = 0; m < M; ++m) {
+        double a = w[m];
+        for (int j = 0; j < m; ++j) a -= sH[m * M + j] * w[j];
+        w[m] = a / sH[m * M + m];
+      }
+      for (int m = M - 1; m >= 0; --m) {
+        double a = w[m];
+        for (int j = m + 1; j < M; ++j) a -= sH[j * M + m] * w[j];
+        w[m] = a / sH[m * M + m];
+      }
+    }
+    lds_sync();
+    // jumps of every reference signal (lanes over time steps); MV bound: half the tighter of the
+    // rate and amplitude ranges (an unbounded MV adds nothing)
+    double e = 0.0;
+    for (int k = 0; k < nref; ++k) {
+      const double* rk = r + (long long)k * my * nit;
+      for (int t = 1 + lane; t < nit; t += kWave) {
+        bool any = false;
+        for (int i = 0; i < my; ++i) any = any || rk[i * nit + t] != rk[i * nit + t - 1];
+        if (!any) continue;
+        for (int n = 0; n < nu; ++n) {
+          const double bn = 0.5 * fmin(sc.bnd[nu + n] - sc.bnd[n], sc.bnd[3 * nu + n] - sc.bnd[2 * nu + n]);
+          if (!(bn > 0.0 && bn < INFINITY)) continue;
+          double s = 0.0;
+          for (int l = 0; l < nuc; ++l) {
+            double z = 0.0;
+            for (int i = 0; i < my; ++i) z += (rk[i * nit + t] - rk[i * nit + t - 1]) * sW[i * M + n * nuc + l];
+            s += fabs(z);
+          }
+          e += s / bn;
+        }
+      }
+    }
+    est = wave_sum64(e);
+  }
+  if (lane == 0) {
+    const double lg = est > 0.0 ? log2(est) : -256.0;
+    const double qd = fmin(fmax((lg + 256.0) * 2048.0, 0.0), 1048575.0);
+    key[c] = ~(((unsigned)M << 20) | (unsigned)(isnan(qd) ? 1048575.0 : qd));
+  }
+}
+
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
-                     const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err) {
+                     const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
+                     const DevScenario* sc, int nref, const double* r) {
   *perm = nullptr;
+#ifdef MPCT_ORDER_IDENTITY  // probe builds: dispatch in the caller's order
+  return 0;
+#endif
   if (C < kOrderMinC) return 0;  // one round of workgroups: the order cannot matter
   if (wo.pending && hipStreamWaitEvent(stream, wo.used, 0) != hipSuccess) {
     *err = "hipStreamWaitEvent failed (dispatch-order buffers)";
@@ -82,8 +228,18 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   unsigned* kout = reinterpret_cast<unsigned*>(b + arr);
   int* iin = reinterpret_cast<int*>(b + 2 * arr);
   int* iout = reinterpret_cast<int*>(b + 3 * arr);
-  hipLaunchKernelGGL(order_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, kind, C, my, nu, N2, Nu,
-                     delta, lambda, kin, iin);
+  // the controller-based estimate when its per-candidate cost (the upper half of H: one
+  // step-table correlation over the horizon per output and entry) stays small; else weight ratio
+  const double hcost = sc ? 0.5 * (double)(sc->nu * sc->numax) * (sc->nu * sc->numax) * sc->my * sc->n2max : 0.0;
+  if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 && hcost <= kOrderEstMaxCost) {
+    const int Mp = sc->nu * sc->numax;
+    const size_t lds = (size_t)(Mp * Mp + sc->my * Mp + sc->my) * sizeof(double);
+    hipLaunchKernelGGL(order_keys_gpc, dim3((unsigned)C), dim3(kWave), lds, stream, *sc, C, nref, N2, Nu, delta,
+                       lambda, r, kin, iin);
+  } else {
+    hipLaunchKernelGGL(order_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, kind, C, my, nu, N2,
+                       Nu, delta, lambda, kin, iin);
+  }
   if (hipcub::DeviceRadixSort::SortPairs(b + 4 * arr, temp, kin, kout, iin, iout, (int)C, 0, 32, stream) !=
       hipSuccess) {
     *err = "hipcub::DeviceRadixSort::SortPairs failed";
