@@ -4,6 +4,10 @@
 #include "wave_ops.h"
 #include "work_order.h"
 
+#ifndef MPCT_KEY_SKIP
+#define MPCT_KEY_SKIP 0  // ablation bits of order_keys_gpc: 1 H build, 2 Cholesky, 4 jump scan
+#endif
+
 namespace mpct {
 
 // ---- dispatch order (longest-processing-time first).  The workgroups of a launch start in slot
@@ -82,26 +86,47 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   double* sH = lds;             // H, then its Cholesky factor L (lower, row-major, stride M)
   double* sW = lds + Mp * Mp;   // w_i (row i, stride M)
   double* sQ = sW + my * Mp;    // q_i
+  double* sS = sQ + my;         // the step table [my][nu][tlen]
+  double* sD = sS + my * nu * tlen;  // jump vectors of one pass [64][my]
+  int* sN1 = reinterpret_cast<int*>(sD + kWave * my);
+  for (int e = lane; e < my * nu * tlen; e += kWave) sS[e] = sc.step[e];
   if (lane < my) {
     const double di = fabs(delta[c * my + lane]);
     const double sqi = sc.wsq ? di : sqrt(di);
     sQ[lane] = sqi * sqi;
+    sN1[lane] = sc.n1[lane];
   }
   lds_sync();
   // H(a,b) = sum_i q_i sum_r G_i(r,a) G_i(r,b) + Lambda,  G_i(r, n*Nu + l) = s_in(n1_i + r - l)
-  for (int e = lane; e < M * M; e += kWave) {
-    const int a = e / M, b = e - a * M;
-    if (b < a) continue;
+  for (int e = lane; e < M * (M + 1) / 2; e += kWave) {  // lanes over the upper triangle
+    int a = 0, b = e;
+    while (b >= M - a) {
+      b -= M - a;
+      ++a;
+    }
+    b += a;
+#if MPCT_KEY_SKIP & 1
+    sH[a * M + b] = a == b ? 1.0 : 0.0;
+    sH[b * M + a] = a == b ? 1.0 : 0.0;
+    continue;
+#endif
     const int na = a / nuc, la = a - na * nuc, nb = b / nuc, lb = b - nb * nuc;
+    const int lm = la > lb ? la : lb;
     double h = 0.0;
     for (int i = 0; i < my; ++i) {
-      const double* sa = sc.step + (long long)(i * nu + na) * tlen;
-      const double* sb = sc.step + (long long)(i * nu + nb) * tlen;
-      const int n1 = sc.n1[i];
-      const int r0 = la > lb ? la - n1 : lb - n1;  // first row where both indices are >= 0
-      double acc = 0.0;
-      for (int rr = r0 > 0 ? r0 : 0; rr < n2; ++rr) acc += sa[n1 + rr - la] * sb[n1 + rr - lb];
-      h += sQ[i] * acc;
+      const int n1 = sN1[i];
+      const double* sa = sS + (i * nu + na) * tlen + n1 - la;  // sa[r] = s_i,na(n1 + r - la)
+      const double* sb = sS + (i * nu + nb) * tlen + n1 - lb;
+      int rr = lm - n1 > 0 ? lm - n1 : 0;  // first row where both step indices are >= 0
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (; rr + 3 < n2; rr += 4) {
+        a0 += sa[rr] * sb[rr];
+        a1 += sa[rr + 1] * sb[rr + 1];
+        a2 += sa[rr + 2] * sb[rr + 2];
+        a3 += sa[rr + 3] * sb[rr + 3];
+      }
+      for (; rr < n2; ++rr) a0 += sa[rr] * sb[rr];
+      h += sQ[i] * ((a0 + a1) + (a2 + a3));
     }
     if (a == b) {
       const double ln = fabs(lambda[c * nu + na]);
@@ -111,19 +136,20 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     sH[a * M + b] = h;
     sH[b * M + a] = h;
   }
-  // right-hand sides q_i G_i'1 (column sums of G_i)
-  for (int e = lane; e < my * M; e += kWave) {
-    const int i = e / M, m = e - i * M, n = m / nuc, l = m - n * nuc;
-    const double* si = sc.step + (long long)(i * nu + n) * tlen;
-    const int n1 = sc.n1[i];
-    double acc = 0.0;
-    for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) acc += si[n1 + rr - l];
-    sW[i * M + m] = sQ[i] * acc;
+  // right-hand sides q_i G_i'1 (column sums of G_i); lane (i, m) keeps its entry in a register
+  const bool wl = lane < my * M;
+  const int wi = wl ? lane / M : 0, wm = wl ? lane - wi * M : 0;
+  double w = 0.0;
+  if (wl) {
+    const int n = wm / nuc, l = wm - n * nuc, n1 = sN1[wi];
+    const double* si = sS + (wi * nu + n) * tlen + n1 - l;
+    for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) w += si[rr];
+    w *= sQ[wi];
   }
   lds_sync();
   // Cholesky H = L L' (lanes over the column below the pivot, then over the trailing block)
   bool spd = true;
-  for (int k = 0; k < M; ++k) {
+  for (int k = 0; k < ((MPCT_KEY_SKIP & 2) ? 0 : M); ++k) {
     const double pk = sH[k * M + k];
     if (!(pk > 0.0)) {
       spd = false;
@@ -142,42 +168,79 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     lds_sync();
   }
   double est = INFINITY;  // a factorisation that fails: treat as heaviest
-  if (spd) {
-    // w_i = H^-1 rhs_i: lane i runs both triangular solves in place
+  if (spd && my * M > kWave) {  // more right-hand side entries than lanes: one lane per output
     if (lane < my) {
-      double* w = sW + lane * M;
+      double* wr = sW + lane * M;
       for (int m = 0; m < M; ++m) {
-        double a = w[m];
-        for (int j = 0; j < m; ++j) a -= sH[m * M + j] * w[j];
-        w[m] = a / sH[m * M + m];
+        const int n = m / nuc, l = m - n * nuc, n1 = sN1[lane];
+        const double* si = sS + (lane * nu + n) * tlen + n1 - l;
+        double acc = 0.0;
+        for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) acc += si[rr];
+        wr[m] = sQ[lane] * acc;
+      }
+      for (int m = 0; m < M; ++m) {
+        double a = wr[m];
+        for (int j = 0; j < m; ++j) a -= sH[m * M + j] * wr[j];
+        wr[m] = a / sH[m * M + m];
       }
       for (int m = M - 1; m >= 0; --m) {
-        double a = w[m];
-        for (int j = m + 1; j < M; ++j) a -= sH[j * M + m] * w[j];
-        w[m] = a / sH[m * M + m];
+        double a = wr[m];
+        for (int j = m + 1; j < M; ++j) a -= sH[j * M + m] * wr[j];
+        wr[m] = a / sH[m * M + m];
       }
     }
     lds_sync();
-    // jumps of every reference signal (lanes over time steps); MV bound: half the tighter of the
-    // rate and amplitude ranges (an unbounded MV adds nothing)
+  } else if (spd) {
+    // w_i = H^-1 rhs_i, lanes over (i, m): forward then backward substitution, the solved entry
+    // of each step handed over in LDS
+    for (int m = 0; m < M; ++m) {
+      if (wl && wm == m) {
+        w /= sH[m * M + m];
+        sW[wi * M + m] = w;
+      }
+      lds_sync();
+      if (wl && wm > m) w -= sH[wm * M + m] * sW[wi * M + m];
+    }
+    for (int m = M - 1; m >= 0; --m) {
+      if (wl && wm == m) {
+        w /= sH[m * M + m];
+        sW[wi * M + m] = w;
+      }
+      lds_sync();
+      if (wl && wm < m) w -= sH[m * M + wm] * sW[wi * M + m];
+    }
+    lds_sync();
+  }
+  if (spd) {
+    // jumps of every reference signal, 64 time steps per pass: lanes flag their step, the jump
+    // vectors of the flagged steps are compacted into LDS (ballot prefix), then lanes over (jump,
+    // move) pairs add |z| / b_n, b_n = half the tighter of MV n's rate and amplitude ranges (an
+    // unbounded MV adds nothing)
     double e = 0.0;
-    for (int k = 0; k < nref; ++k) {
+    for (int k = 0; k < ((MPCT_KEY_SKIP & 4) ? 0 : nref); ++k) {
       const double* rk = r + (long long)k * my * nit;
-      for (int t = 1 + lane; t < nit; t += kWave) {
-        bool any = false;
-        for (int i = 0; i < my; ++i) any = any || rk[i * nit + t] != rk[i * nit + t - 1];
-        if (!any) continue;
-        for (int n = 0; n < nu; ++n) {
+      for (int t0 = 1; t0 < nit; t0 += kWave) {
+        const int t = t0 + lane;
+        bool jmp = false;
+        if (t < nit)
+          for (int i = 0; i < my; ++i) jmp = jmp || rk[i * nit + t] != rk[i * nit + t - 1];
+        const unsigned long long bal = __ballot(jmp);
+        if (!bal) continue;
+        if (jmp) {
+          const int slot = __popcll(bal & ((1ull << lane) - 1ull));
+          for (int i = 0; i < my; ++i) sD[slot * my + i] = rk[i * nit + t] - rk[i * nit + t - 1];
+        }
+        lds_sync();
+        const int nj = __popcll(bal);
+        for (int p = lane; p < nj * M; p += kWave) {
+          const int j = p / M, m = p - j * M, n = m / nuc;
           const double bn = 0.5 * fmin(sc.bnd[nu + n] - sc.bnd[n], sc.bnd[3 * nu + n] - sc.bnd[2 * nu + n]);
           if (!(bn > 0.0 && bn < INFINITY)) continue;
-          double s = 0.0;
-          for (int l = 0; l < nuc; ++l) {
-            double z = 0.0;
-            for (int i = 0; i < my; ++i) z += (rk[i * nit + t] - rk[i * nit + t - 1]) * sW[i * M + n * nuc + l];
-            s += fabs(z);
-          }
-          e += s / bn;
+          double z = 0.0;
+          for (int i = 0; i < my; ++i) z += sD[j * my + i] * sW[i * M + m];
+          e += fabs(z) / bn;
         }
+        lds_sync();
       }
     }
     est = wave_sum64(e);
@@ -231,9 +294,12 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   // the controller-based estimate when its per-candidate cost (the upper half of H: one
   // step-table correlation over the horizon per output and entry) stays small; else weight ratio
   const double hcost = sc ? 0.5 * (double)(sc->nu * sc->numax) * (sc->nu * sc->numax) * sc->my * sc->n2max : 0.0;
-  if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 && hcost <= kOrderEstMaxCost) {
+  const long long ldsd = sc ? (long long)(sc->nu * sc->numax) * (sc->nu * sc->numax) + (long long)sc->my * sc->nu * sc->tlen : 0;
+  if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 && hcost <= kOrderEstMaxCost &&
+      ldsd <= 6144) {
     const int Mp = sc->nu * sc->numax;
-    const size_t lds = (size_t)(Mp * Mp + sc->my * Mp + sc->my) * sizeof(double);
+    const size_t lds = (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) * sizeof(double) +
+                       (size_t)sc->my * sizeof(int);
     hipLaunchKernelGGL(order_keys_gpc, dim3((unsigned)C), dim3(kWave), lds, stream, *sc, C, nref, N2, Nu, delta,
                        lambda, r, kin, iin);
   } else {
