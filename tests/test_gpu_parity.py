@@ -154,6 +154,46 @@ def test_full_grid_properties(env):
     assert np.array_equal(rank(a.J1 @ w), rank(ref["J1"] @ w))
 
 
+def test_dispatch_key_mixed_horizons_and_step_refs(built):
+    """The controller-based dispatch key (work_order.hip order_keys_gpc) runs for batches of >= 256
+    candidates. Cover both of its solve paths: lanes over (output, move) when my*M <= 64, and one
+    lane per output when my*M > 64 (Nu = 8: M = 24). Include bad horizons and the VNS step
+    references (nref = 3). The order must not change any result: compare with the C port, and
+    with the same batch reversed."""
+    from mpct.engine import eval_batch
+    from mpct.scenarios import shell3x3, vns_step_refs
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3
+
+    rng = np.random.default_rng(7)
+    C = 320
+    N2 = rng.integers(8, 31, size=C).astype(np.int32)
+    Nu = np.minimum(rng.integers(1, 9, size=C), N2).astype(np.int32)
+    N2[:4] = (0, 31, 5, 12)  # skipped, N2 > n2_max, Nu > N2, valid
+    Nu[:4] = (3, 2, 7, 8)
+    d = 10.0 ** rng.uniform(-3, 0, size=(C, 3))
+    l = 10.0 ** rng.uniform(-4, -1, size=(C, 3))
+    sc, r, yref = shell3x3(n2_max=30, nu_max=8, nit=150)
+    osc, orr, oyref, _ = o_shell3x3()
+    cp = CPort(osc, 30, 150, np.ascontiguousarray(oyref[:, :150]))
+    for refs, orefs in ((r[None], orr[None, :, :150]), (vns_step_refs(3, 150), vns_step_refs(3, 150))):
+        res = eval_batch(sc, N2, Nu, d, l, refs)
+        rev = eval_batch(sc, N2[::-1].copy(), Nu[::-1].copy(), d[::-1].copy(), l[::-1].copy(), refs)
+        ref = cp.eval(N2, Nu, d, l, orefs, threads=8)
+        st = res.status.reshape(C, -1)
+        assert np.all(st[0] == 8) and np.all(st[1] == 16) and np.all(st[2] == 16)
+        assert np.array_equal(st, rev.status.reshape(C, -1)[::-1])
+        assert np.array_equal(res.J1, rev.J1.reshape(C, -1, 3)[::-1].reshape(res.J1.shape), equal_nan=True)
+        # unit steps drive a few aggressive candidates into the QP iteration cap (status 1) on
+        # both sides; compare the simulations that are clean on both
+        cst = np.asarray(ref["status"]).reshape(C, -1)
+        ok = np.all(st == 0, axis=1) & np.all(cst == 0, axis=1)
+        assert ok[3:].mean() > 0.97, ok[3:].mean()
+        a = res.J1.reshape(C, -1)[ok]
+        b = np.asarray(ref["J1"]).reshape(C, -1)[ok]
+        assert _rel(a, b) < COST_RTOL, _rel(a, b)
+
+
 def test_status_edges(env):
     from mpct.engine import eval_batch
 
