@@ -147,8 +147,10 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     w *= sQ[wi];
   }
   lds_sync();
-  // Cholesky H = L L' (lanes over the column below the pivot, then over the trailing block)
+  // Cholesky H = L L': lane i owns row i (column k below the pivot, then its row of the
+  // trailing block; no integer division in the loop)
   bool spd = true;
+  const bool hr = lane < M;
   for (int k = 0; k < ((MPCT_KEY_SKIP & 2) ? 0 : M); ++k) {
     const double pk = sH[k * M + k];
     if (!(pk > 0.0)) {
@@ -157,14 +159,15 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     }
     const double lk = sqrt(pk), il = 1.0 / lk;
     lds_sync();
-    for (int i = k + 1 + lane; i < M; i += kWave) sH[i * M + k] *= il;
-    if (lane == 0) sH[k * M + k] = lk;
-    lds_sync();
-    const int t = M - k - 1;
-    for (int e = lane; e < t * t; e += kWave) {
-      const int i = k + 1 + e / t, j = k + 1 + e % t;
-      if (j <= i) sH[i * M + j] -= sH[i * M + k] * sH[j * M + k];
+    double lik = 0.0;
+    if (lane == k) sH[k * M + k] = lk;
+    if (hr && lane > k) {
+      lik = sH[lane * M + k] * il;
+      sH[lane * M + k] = lik;
     }
+    lds_sync();
+    if (hr && lane > k)
+      for (int j = k + 1; j <= lane; ++j) sH[lane * M + j] -= lik * sH[j * M + k];
     lds_sync();
   }
   double est = INFINITY;  // a factorisation that fails: treat as heaviest
