@@ -4,6 +4,10 @@
 #include "wave_ops.h"
 #include "work_order.h"
 
+#ifndef MPCT_NMPC_KEY
+#define MPCT_NMPC_KEY 1  // NMPC dispatch key: 1 N Nu; 2 N Nu, then the weight ratio; 0 log(N Nu) - 0.1 a
+                         // (config 5 GAM mode: 267 / 267 / 288 ms, tools/diag/nmpc_order_ab.py)
+#endif
 #ifndef MPCT_KEY_SKIP
 #define MPCT_KEY_SKIP 0  // ablation bits of order_keys_gpc: 1 H build, 2 Cholesky, 4 jump scan
 #endif
@@ -20,10 +24,11 @@ namespace mpct {
 // grid order 5.36 ms, this key 3.9 ms, ideal (measured QP work, descending) 3.58 ms.  GPC and
 // DTC-GPC batches now use the controller-based estimate of order_keys_gpc below; this weight-ratio
 // key remains for NMPC and for scenarios whose H is too large to form per candidate.
-// NMPC (config 5, tools/order_probe5.py, tools/nmpc_key_ab.sh): the Gauss-Newton iteration count
-// falls as the weight ratio grows (Spearman -0.54) while the work per iteration grows with the
-// horizon N and the QP size; score log(N Nu) - 0.1 a.  Closed loop of the 4096 grid: grid order
-// 506 ms, N Nu order 376 ms, this score 367 ms, ideal (measured work) 345 ms.
+// NMPC (config 5, tools/order_probe5.py, tools/diag/nmpc_order_ab.py): the work per Gauss-Newton
+// iteration grows with the horizon N and the QP size.  Since the Anderson-accelerated iteration
+// (round 2), N Nu alone orders the batch as well as the measured work (GAM mode: 267 ms for both,
+// grid order 331 ms); the round-1 score log(N Nu) - 0.1 a, which also weighed the iteration
+// count, now costs 288 ms (MPCT_NMPC_KEY).
 __global__ void order_keys(int kind, long long C, int my, int nu, const int* __restrict__ N2,
                            const int* __restrict__ Nu, const double* __restrict__ delta,
                            const double* __restrict__ lambda, unsigned* __restrict__ key, int* __restrict__ idx) {
@@ -38,12 +43,17 @@ __global__ void order_keys(int kind, long long C, int my, int nu, const int* __r
     double a = 0.0;
     for (int j = 0; j < nu; ++j) a += log2(fmax(dmax, 1e-300) / fmax(fabs(lambda[c * nu + j]), 1e-300));
     a /= nu;
-    if (kind == kOrderNmpc) {
+    if (kind == kOrderNmpc && MPCT_NMPC_KEY == 0) {
       // heavier = larger score; map the float score to an order-preserving unsigned, inverted
       const float sc = (float)(log((double)n2 * nuc) - 0.1 * a);
       unsigned u = __float_as_uint(sc);
       u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
       k = ~u;
+    } else if (kind == kOrderNmpc) {
+      // N * Nu first (the prediction's length times the QP size), then, with MPCT_NMPC_KEY 2,
+      // the smaller weight ratio first (more Gauss-Newton iterations)
+      const double qa = MPCT_NMPC_KEY == 2 ? fmin(fmax((256.0 - a) * 32.0, 0.0), 16383.0) : 0.0;
+      k = ~(((unsigned)(n2 * nuc) << 14) | (unsigned)qa);
     } else {
       const double qd = fmin(fmax((a + 256.0) * 2048.0, 0.0), 1048575.0);
       const unsigned M = (unsigned)(nu * nuc);
