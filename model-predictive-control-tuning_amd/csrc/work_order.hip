@@ -4,6 +4,9 @@
 #include "wave_ops.h"
 #include "work_order.h"
 
+#ifndef MPCT_GPC_EST
+#define MPCT_GPC_EST 1  // GPC / DTC-GPC batches keyed by order_keys_gpc (0: the weight-ratio key)
+#endif
 #ifndef MPCT_NMPC_KEY
 #define MPCT_NMPC_KEY 1  // NMPC dispatch key: 1 N Nu; 2 N Nu, then the weight ratio; 0 log(N Nu) - 0.1 a
                          // (config 5 GAM mode: 267 / 267 / 288 ms, tools/diag/nmpc_order_ab.py)
@@ -308,7 +311,8 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   // step-table correlation over the horizon per output and entry) stays small; else weight ratio
   const double hcost = sc ? 0.5 * (double)(sc->nu * sc->numax) * (sc->nu * sc->numax) * sc->my * sc->n2max : 0.0;
   const long long ldsd = sc ? (long long)(sc->nu * sc->numax) * (sc->nu * sc->numax) + (long long)sc->my * sc->nu * sc->tlen : 0;
-  if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 && hcost <= kOrderEstMaxCost &&
+  if (MPCT_GPC_EST && kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 &&
+      hcost <= kOrderEstMaxCost &&
       ldsd <= 6144) {
     const int Mp = sc->nu * sc->numax;
     const size_t lds = (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) * sizeof(double) +
