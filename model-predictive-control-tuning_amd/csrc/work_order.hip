@@ -310,18 +310,22 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   // the controller-based estimate when its per-candidate cost (the upper half of H: one
   // step-table correlation over the horizon per output and entry) stays small; else weight ratio
   const double hcost = sc ? 0.5 * (double)(sc->nu * sc->numax) * (sc->nu * sc->numax) * sc->my * sc->n2max : 0.0;
-  const long long ldsd = sc ? (long long)(sc->nu * sc->numax) * (sc->nu * sc->numax) + (long long)sc->my * sc->nu * sc->tlen : 0;
-  if (MPCT_GPC_EST && kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && sc->nu * sc->numax <= 64 &&
-      hcost <= kOrderEstMaxCost &&
-      ldsd <= 6144) {
-    const int Mp = sc->nu * sc->numax;
-    const size_t lds = (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) * sizeof(double) +
-                       (size_t)sc->my * sizeof(int);
+  const int Mp = sc ? sc->nu * sc->numax : 0;
+  const size_t lds = sc ? (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) *
+                                  sizeof(double) + (size_t)sc->my * sizeof(int)
+                        : 0;
+  if (MPCT_GPC_EST && kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && Mp <= 64 &&
+      hcost <= kOrderEstMaxCost && lds <= 64 * 1024) {
     hipLaunchKernelGGL(order_keys_gpc, dim3((unsigned)C), dim3(kWave), lds, stream, *sc, C, nref, N2, Nu, delta,
                        lambda, r, kin, iin);
   } else {
     hipLaunchKernelGGL(order_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, kind, C, my, nu, N2,
                        Nu, delta, lambda, kin, iin);
+  }
+  const hipError_t ke = hipGetLastError();
+  if (ke != hipSuccess) {
+    *err = std::string("dispatch-order key launch failed: ") + hipGetErrorString(ke);
+    return -3;
   }
   if (hipcub::DeviceRadixSort::SortPairs(b + 4 * arr, temp, kin, kout, iin, iout, (int)C, 0, 32, stream) !=
       hipSuccess) {
