@@ -291,6 +291,13 @@ int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const int32_t* dev
  * mpct_eval_batch_multi and of the torch.distributed ranks).  Returns *hi - *lo, or <0. */
 int64_t mpct_shard_range(int64_t C, int32_t ndev, int32_t k, int64_t* lo, int64_t* hi);
 
+/* The ranking every rank computes after the cost all-gather (Shell3x3.m:161 ranks by
+ * the Pareto-weighted cost): perm[0..C) = candidate indices by ascending s_c = sum_j costs[c*k+j] *
+ * w[j], ties by candidate index, NaN costs (failed / sentinel candidates) last.  All pointers are
+ * DEVICE pointers; enqueued on `stream` (NULL = default), not synchronised.  One key kernel and a
+ * device radix sort (stable).  Returns MPCT_OK or <0. */
+int32_t mpct_rank_device(const double* costs, int64_t C, int32_t k, const double* w, int32_t* perm, void* stream);
+
 /* Name of the kernel instance mpct_eval_batch(_device) launches for this scenario and options,
  * e.g. "gpc_closed_loop_kernel<16,false,false>" (QP-size class, DTC mode, open-loop/trajectory
  * state).  Copies at most cap-1 characters plus a NUL into buf; returns the name's length, or <0.

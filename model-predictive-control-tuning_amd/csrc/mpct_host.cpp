@@ -961,6 +961,17 @@ extern "C" int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int
   return launch_batch(s, cx, C, N2, Nu, delta, lambda, nref, r, v, opts, out, static_cast<hipStream_t>(stream));
 }
 
+extern "C" int32_t mpct_rank_device(const double* costs, int64_t C, int32_t k, const double* w, int32_t* perm,
+                                    void* stream) {
+  if (C < 0 || C > 2147483647LL) return fail(MPCT_ERANGE, "C out of range for the ranking sort");
+  if (k < 1) return fail(MPCT_EINVAL, "k < 1");
+  if (C > 0 && (!costs || !w || !perm)) return fail(MPCT_EINVAL, "null pointer");
+  std::string err;
+  const int rc = rank_device(costs, C, k, w, perm, static_cast<hipStream_t>(stream), &err);
+  if (rc) return fail(rc == -2 ? MPCT_ENOMEM : MPCT_EDEVICE, err);
+  return MPCT_OK;
+}
+
 // host buffers in, host buffers out, on the context's own stream: H2D of the candidates and
 // signals, the launch, D2H of the results, then a wait on that stream only
 static int eval_host(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* N2, const int32_t* Nu,

@@ -30,6 +30,10 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
                      const DevScenario* sc = nullptr, int nref = 0, const double* r = nullptr);
 
+// ascending weighted-cost order of C candidates (mpct_rank_device): device pointers, on `stream`
+int rank_device(const double* costs, long long C, int k, const double* w, int* perm, hipStream_t stream,
+                std::string* err);
+
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);
 void order_release(WorkOrder& wo);

@@ -336,6 +336,57 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   return 0;
 }
 
+// ---- ranking (mpct_rank_device): s_c = sum_j costs[c][j] w[j] in a fixed order, NaN -> +inf,
+// -0 -> +0, mapped to an order-preserving unsigned 64-bit key; the radix sort is stable, so equal
+// costs keep the candidate order
+__global__ void rank_keys(const double* __restrict__ costs, long long C, int k, const double* __restrict__ w,
+                          unsigned long long* __restrict__ key, int* __restrict__ idx) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int j = 0; j < k; ++j) s = fma(costs[c * k + j], w[j], s);
+  if (isnan(s)) s = INFINITY;
+  s += 0.0;  // -0 -> +0 (round to nearest)
+  unsigned long long u = (unsigned long long)__double_as_longlong(s);
+  u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  key[c] = u;
+  idx[c] = (int)c;
+}
+
+int rank_device(const double* costs, long long C, int k, const double* w, int* perm, hipStream_t stream,
+                std::string* err) {
+  if (C == 0) return 0;
+  size_t temp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned long long*)nullptr,
+                                         (unsigned long long*)nullptr, (const int*)nullptr, (int*)nullptr,
+                                         (int)C) != hipSuccess) {
+    *err = "hipcub::DeviceRadixSort::SortPairs (size query) failed";
+    return -3;
+  }
+  const size_t arr8 = ((size_t)C * 8 + 255) & ~(size_t)255, arr4 = ((size_t)C * 4 + 255) & ~(size_t)255;
+  void* buf = nullptr;
+  if (hipMallocAsync(&buf, 2 * arr8 + arr4 + temp, stream) != hipSuccess) {
+    *err = "hipMallocAsync failed (ranking buffers)";
+    return -2;
+  }
+  char* b = static_cast<char*>(buf);
+  unsigned long long* kin = reinterpret_cast<unsigned long long*>(b);
+  unsigned long long* kout = reinterpret_cast<unsigned long long*>(b + arr8);
+  int* iin = reinterpret_cast<int*>(b + 2 * arr8);
+  hipLaunchKernelGGL(rank_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, costs, C, k, w, kin, iin);
+  int rc = 0;
+  if (hipGetLastError() != hipSuccess) {
+    *err = "ranking key launch failed";
+    rc = -3;
+  } else if (hipcub::DeviceRadixSort::SortPairs(b + 2 * arr8 + arr4, temp, kin, kout, iin, perm, (int)C, 0, 64,
+                                                stream) != hipSuccess) {
+    *err = "hipcub::DeviceRadixSort::SortPairs failed (ranking)";
+    rc = -3;
+  }
+  (void)hipFreeAsync(buf, stream);
+  return rc;
+}
+
 void order_release(WorkOrder& wo) {
   if (wo.buf) (void)hipFree(wo.buf);
   if (wo.used) (void)hipEventDestroy(wo.used);

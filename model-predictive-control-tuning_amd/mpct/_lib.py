@@ -85,6 +85,7 @@ EXPORTS = [
     "mpct_abi_version", "mpct_last_error", "mpct_scenario_create", "mpct_scenario_destroy",
     "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
     "mpct_nmpc_scenario_create", "mpct_eval_batch_multi", "mpct_shard_range", "mpct_kernel_instance",
+    "mpct_rank_device",
 ]
 
 ABI_VERSION = 5
@@ -144,6 +145,8 @@ def load():
     lib.mpct_shard_range.restype = C.c_int64
     lib.mpct_kernel_instance.argtypes = [C.c_void_p, C.POINTER(MpctOpts), C.c_char_p, C.c_int32]
     lib.mpct_kernel_instance.restype = C.c_int32
+    lib.mpct_rank_device.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.mpct_rank_device.restype = C.c_int32
     if lib.mpct_abi_version() != ABI_VERSION:
         raise ImportError("libmpct ABI version mismatch")
     _lib = lib

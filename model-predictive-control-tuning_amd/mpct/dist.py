@@ -49,9 +49,23 @@ def gather_costs(local: torch.Tensor, group=None) -> torch.Tensor:
 def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = None) -> torch.Tensor:
     """Candidate order by ascending weighted cost (Shell3x3.m:161 Pareto weights), ties by
     candidate index; NaN costs (failed / sentinel candidates) sort last.  Identical on every
-    rank because every rank sorts the same gathered tensor."""
-    s = costs @ weights
+    rank because every rank sorts the same gathered tensor.  GPU tensors go through the
+    library's mpct_rank_device (one key kernel + a stable device radix sort on the current
+    stream); CPU tensors (the gloo tests) through torch."""
     if C is not None:
-        s = s[:C]
+        costs = costs[:C]
+    if costs.is_cuda:
+        from . import _lib
+
+        c = costs.to(torch.float64).contiguous()
+        w = weights.to(device=c.device, dtype=torch.float64).contiguous()
+        perm = torch.empty(c.shape[0], dtype=torch.int32, device=c.device)
+        stream = torch.cuda.current_stream(c.device).cuda_stream
+        rc = _lib.load().mpct_rank_device(c.data_ptr(), c.shape[0], c.shape[1], w.data_ptr(), perm.data_ptr(),
+                                          stream)
+        if rc != 0:
+            raise RuntimeError("mpct_rank_device failed (%d): %s" % (rc, _lib.load().mpct_last_error().decode()))
+        return perm.to(torch.int64)
+    s = costs @ weights
     s = torch.where(torch.isnan(s), torch.full_like(s, float("inf")), s)
     return torch.argsort(s, stable=True)

@@ -194,6 +194,36 @@ def test_dispatch_key_mixed_horizons_and_step_refs(built):
         assert _rel(a, b) < COST_RTOL, _rel(a, b)
 
 
+def test_rank_device_matches_stable_sort(built):
+    """mpct_rank_device (the ranking after the cost all-gather, mpct.dist.rank_candidates on GPU
+    tensors) against a stable CPU sort of the same rule.  Costs are small integers and weights powers
+    of two, so every weighted sum is exact and the expected order is unambiguous. The rows include
+    ties, NaN costs (last, by index), +-inf, and -0 next to +0."""
+    import torch
+
+    from mpct.dist import rank_candidates
+
+    rng = np.random.default_rng(3)
+    C = 5000
+    costs = rng.integers(0, 40, size=(C, 3)).astype(float)
+    costs[rng.integers(0, C, 60), rng.integers(0, 3, 60)] = np.nan
+    costs[10] = (np.inf, 0.0, 0.0)
+    costs[11] = (-np.inf, 0.0, 0.0)
+    costs[12] = (-0.0, -0.0, -0.0)
+    costs[13] = (0.0, 0.0, 0.0)
+    costs[14] = costs[13]
+    w = np.array([0.5, 0.25, 1.0])
+    s = costs @ w
+    s[np.isnan(s)] = np.inf
+    expect = np.argsort(s, kind="stable")
+    dev = torch.device("cuda", 0)
+    got = rank_candidates(torch.from_numpy(costs).to(dev), torch.from_numpy(w).to(dev)).cpu().numpy()
+    assert np.array_equal(got, expect)
+    # the C = prefix form used by the padded multi-rank batch
+    got2 = rank_candidates(torch.from_numpy(costs).to(dev), torch.from_numpy(w).to(dev), C=3000).cpu().numpy()
+    assert np.array_equal(got2, np.argsort(s[:3000], kind="stable"))
+
+
 def test_status_edges(env):
     from mpct.engine import eval_batch
 
