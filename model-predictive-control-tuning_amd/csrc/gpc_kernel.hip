@@ -38,6 +38,16 @@
 #ifndef MPCT_REG_Y
 #define MPCT_REG_Y 0   // y backward-difference histories in VGPRs (else in LDS; 0 measured faster)
 #endif
+#ifndef MPCT_EXP_SKIP
+#define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
+#endif
+#ifndef MPCT_PRIO
+#define MPCT_PRIO 0  // wave issue priority for the heaviest slots (1: top 1/16, 2: graded 1/16, 1/4, 1/2)
+#endif
+#ifndef MPCT_UUPD_DEFER
+#define MPCT_UUPD_DEFER 0  // the u update of step t at the top of step t+1 (one LDS hand-off fewer per step)
+#endif
+
 namespace mpct {
 
 struct LdsLayout {
@@ -121,6 +131,15 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const int kref = (int)(slot - cs * nref);
   const long long c = perm ? (long long)perm[cs] : cs;
   const long long sim = c * nref + kref;
+#if MPCT_PRIO
+  // issue priority by estimated work: the heaviest slots of an ordered launch (experiment knob)
+  if (perm) {
+    const long long tot = C * nref;
+    if (slot < tot / 16) __builtin_amdgcn_s_setprio(3);
+    else if (MPCT_PRIO > 1 && slot < tot / 4) __builtin_amdgcn_s_setprio(2);
+    else if (MPCT_PRIO > 1 && slot < tot / 2) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
   const int my = sc.my, nu = sc.nu, nin = sc.nin, nit = sc.nit, nx = sc.nx, ne = sc.ne;
   const int N2 = N2v[c], Nu = Nuv[c];
   const int M = nu * Nu;
@@ -451,12 +470,44 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     r_t = rr[lane * nit];
     yr_t = sc.yref[lane * nit];
   }
+  // u(t) = u(t-1) + du(t, first move) of MV n = lane: past-control state, plant input ring
+  auto u_update = [&](int t, int ln) __attribute__((always_inline)) {
+    if (!(MPCT_EXP_SKIP & 8) && ln < nu) {
+      const int n = lane;
+      const double du = sxc[n * Nu];
+      const double un = suprev[n] + du;
+      if (regpath && MPCT_REG_DU) {  // past-control register in registers, written out whole
+#pragma unroll
+        for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
+        duh[0] = du;
+#pragma unroll
+        for (int k = 0; k < kRegDu; ++k)
+          if (k < dum_n) sx[upoff_n + k] = duh[k];
+      } else {
+        for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
+        sx[upoff_n] = du;
+      }
+      sur[n * kURing + (t & (kURing - 1))] = un;
+      if ((EXT && o.want_traj)) {
+        if (out.u) out.u[(sim * nu + n) * nit + t] = un;
+        if ((EXT && o.open_loop) && out.uopt) {
+          const int l = t < Nu - 1 ? t : Nu - 1;
+          // Info.Uopt has p+1 rows then the padding repeats the last row (:94-98)
+          out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
+        }
+      }
+      suprev[n] = un;
+    }
+  };
   for (int t = 0; t < nit; ++t) {
     // the lane predicates of the step are re-derived from an opaque copy of the lane id every
     // step: hoisted out of the loop they are kept as SGPR-pair exec masks, which the kernel's
     // SGPR budget spills to VGPR lanes and reloads (v_readlane) several times per step
     int ln = lane;
     asm volatile("" : "+v"(ln));
+    // MPCT_UUPD_DEFER: step t-1's u update runs here, under the same LDS hand-off as the inputs
+    // of step t (sxc still holds step t-1's moves: nothing writes it before the next solve)
+    if (MPCT_UUPD_DEFER && t > 0) u_update(t - 1, ln);
     double r_n = 0.0, yr_n = 0.0;
     if (lane < my && t + 1 < nit) {  // prefetch t+1
       r_n = rr[lane * nit + t + 1];
@@ -475,9 +526,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-#ifndef MPCT_EXP_SKIP
-#define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
-#endif
     if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
@@ -590,36 +638,17 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     lds_sync();
     PSTAMP(PROF_YUPD);
     if (!(MPCT_EXP_SKIP & 4)) solve_step();
-    if (!(MPCT_EXP_SKIP & 8) && ln < nu) {
-      const int n = lane;
-      const double du = sxc[n * Nu];
-      const double un = suprev[n] + du;
-      if (regpath && MPCT_REG_DU) {  // past-control register in registers, written out whole
-#pragma unroll
-        for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
-        duh[0] = du;
-#pragma unroll
-        for (int k = 0; k < kRegDu; ++k)
-          if (k < dum_n) sx[upoff_n + k] = duh[k];
-      } else {
-        for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
-        sx[upoff_n] = du;
-      }
-      sur[n * kURing + (t & (kURing - 1))] = un;
-      if ((EXT && o.want_traj)) {
-        if (out.u) out.u[(sim * nu + n) * nit + t] = un;
-        if ((EXT && o.open_loop) && out.uopt) {
-          const int l = t < Nu - 1 ? t : Nu - 1;
-          // Info.Uopt has p+1 rows then the padding repeats the last row (:94-98)
-          out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
-        }
-      }
-      suprev[n] = un;
+    if (!MPCT_UUPD_DEFER) {
+      u_update(t, ln);
+      lds_sync();
     }
-    lds_sync();
     r_t = r_n;
     yr_t = yr_n;
     PSTAMP(PROF_UUPD);
+  }
+  if (MPCT_UUPD_DEFER && nit > 0) {
+    int ln = lane;
+    u_update(nit - 1, ln);
   }
 #ifdef MPCT_PROFILE
   if (lane == 0 && out.prof)
