@@ -82,7 +82,7 @@ __device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
 template <int MAXM>
 __device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
                                              bool row) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   if (row)
     for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
   S.nrot = 0;
@@ -94,7 +94,7 @@ __device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, cons
 template <int MAXM>
 __device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, int j0, int mp, double sg,
                                           bool row) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   double dk = 0.0;
   if (row) {
     for (int j = j0; j <= mp; ++j) dk += sJT[lane * M + j];
@@ -106,7 +106,7 @@ __device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, 
 
 // z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
 __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   double z0 = 0.0, z1 = 0.0;
   if (row) {
     int k = q;
@@ -122,7 +122,7 @@ __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int 
 // r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
 template <int MAXM>
 __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   double ck = lane < S.q ? c : 0.0, rk = 0.0;
 #if MPCT_BACKSUB_PIPE
   // the next column's R_A entry is loaded one step ahead, so its LDS latency overlaps this
@@ -155,7 +155,7 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
 // removes row kd, since (G R_A E)^-1 = rows != kd of (R_A^-1 G').  Rebuilt with J.
 // r_w = sum_{c<q} B(w,c) v_c  (lane w < q; v in LDS, synchronised by the caller)
 __device__ __forceinline__ double gi_bdot(const double* sB, const double* sv, int q, int M) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   double a0 = 0.0, a1 = 0.0;
   if (lane < q) {
     const double* b = sB + lane * M;
@@ -170,7 +170,7 @@ __device__ __forceinline__ double gi_bdot(const double* sB, const double* sv, in
 }
 // w_k = sum_{w<=k} B(w,k) v_w  (lane k < q): B'v
 __device__ __forceinline__ double gi_btdot(const double* sB, const double* sv, int q, int M) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   double a0 = 0.0, a1 = 0.0;
   if (lane < q) {
     int w = 0;
@@ -189,7 +189,7 @@ template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
                                        const Mark& mark, double* sB = nullptr, double rk = 0.0) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   const int q = S.q;
   const double dq = bcast(dk, q);
   const double nrm = MPCT_QP_FASTDIV ? beta * rsq_nr(beta) : sqrt(beta);  // beta > 0 on an add
@@ -227,7 +227,7 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
 template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
                                         const Mark& mark, double* sB = nullptr) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);

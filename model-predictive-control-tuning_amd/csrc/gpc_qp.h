@@ -43,7 +43,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
                      , unsigned long long* pacc, unsigned long long& pprev
 #endif
                      ) {
-  const int lane = threadIdx.x;
+  const int lane = qp_lane();
   const bool row = lane < M;
   const double* sRi = Q.rinv;
   double* sxc = Q.xc;
@@ -54,10 +54,12 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
   double* sB = MPCT_GI_B ? Q.b : nullptr;
   double* sw = Q.w;
   if (!row) up_row = 0.0;
+  int rl = rc.l;  // the lane's position in its MV block
+  if (MPCT_QP_OPAQUE) asm volatile("" : "+v"(rl));
   const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
   auto slacks = [&](double x, double s[4]) {
-    const double pre = block_prefix<MAXM>(x, rc.l, Nu, row, sxc);
-    if (rc.l == 0) {
+    const double pre = block_prefix<MAXM>(x, rl, Nu, row, sxc);
+    if (rl == 0) {
       s[0] = x - lo_box;
       s[1] = hi_box - x;
       s[2] = INFINITY;

@@ -37,6 +37,17 @@ __device__ __forceinline__ double rsq_nr(double x) {
   return r * fma(-h * r, r, 1.5);
 }
 
+#ifndef MPCT_QP_OPAQUE
+#define MPCT_QP_OPAQUE 0  // QP lane predicates from an opaque lane id (not hoisted out of the step loop)
+#endif
+// lane id for the QP helpers: with MPCT_QP_OPAQUE an opaque copy, so the compiler re-derives the
+// loop-invariant lane predicates where they are used instead of keeping them as SGPR-pair masks
+__device__ __forceinline__ int qp_lane() {
+  int l = threadIdx.x;
+  if (MPCT_QP_OPAQUE) asm volatile("" : "+v"(l));
+  return l;
+}
+
 __device__ __forceinline__ double bcast(double v, int src) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
