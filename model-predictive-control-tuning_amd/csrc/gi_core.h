@@ -54,7 +54,7 @@ struct RowCons {
 // lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
 // and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
 // convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
-// R^-1 (re-adding the set) after MPCT_GI_REBUILD * M rotations (gpc_qp.h, 8M), which bounds the
+// R^-1 (re-adding the set) after MPCT_GI_REBUILD * M rotations (gpc_qp.h, 32M), which bounds the
 // orthogonality drift of the rotated J (unbounded drift measured 3.5e-5 relative on the metric
 // grid; with the rebuild 7.5e-10).
 template <int MAXM>

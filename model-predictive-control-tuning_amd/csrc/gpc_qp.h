@@ -13,8 +13,8 @@
 #endif
 
 #ifndef MPCT_GI_REBUILD
-#define MPCT_GI_REBUILD 8  // J (and R_A) rebuilt from R^-1 after this many x M rotations (DESIGN.md §5;
-                           // 8 M: 5 % faster than 4 M on the metric grid, same parity, tools/ab_variants.sh)
+#define MPCT_GI_REBUILD 32  // J (and R_A) rebuilt from R^-1 after this many x M rotations (DESIGN.md §5;
+                            // 8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than 8 M; same parity, tools/ab_variants.sh)
 #endif
 
 namespace mpct {
