@@ -177,7 +177,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
           bid = 4 * lane + k;
         }
     }
-    qargmin<MAXM>(best, bid);
+    qargmin<MAXM>(best, bid, 2);
     PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
     if (it >= maxit || S.q >= M) {
@@ -209,7 +209,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
         t1 = qp_div(S.uw, rk);
         kdrop = lane;
       }
-      qargmin<MAXM>(t1, kdrop);
+      qargmin<MAXM>(t1, kdrop, 0);
       PSTAMP(PROF_QR);
       const double t2 = (beta > 1e-14 * dn2) ? -qp_div(sp, beta) : INFINITY;
       if (t1 == INFINITY && t2 == INFINITY) {

@@ -128,9 +128,48 @@ __device__ __forceinline__ double qsum(double v) {
     return wave_sum64(v);
   }
 }
+#ifndef MPCT_PACKED_ARGMIN
+#define MPCT_PACKED_ARGMIN 1  // M <= 16 argmin on one order-preserving 64-bit key (value bits | id)
+#endif
+// (v, id) -> one unsigned key whose order is v's order, with v's low 6 mantissa bits replaced by
+// id (< 64): one u64 compare per DPP step instead of the (value, id) pair.  The winner's exact
+// value is re-read from its lane (ids are 4 * lane + k or lane: lane = id >> shift).
+__device__ __forceinline__ unsigned long long argkey(double v, int id) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long u = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+  return (u & ~63ull) | (unsigned long long)(id & 63);
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dppu64(unsigned long long k) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)k, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(k >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long row_minkey(unsigned long long k) {
+  k = min(k, dppu64<kQx1>(k));
+  k = min(k, dppu64<kQx2>(k));
+  k = min(k, dppu64<kHalfMirror>(k));
+  k = min(k, dppu64<kMirror>(k));
+  return k;
+}
+
 template <int MAXM>
-__device__ __forceinline__ void qargmin(double& v, int& id) {
+__device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
   if constexpr (MAXM <= 16) {
+    if (MPCT_PACKED_ARGMIN && shift >= 0) {
+      // lanes >= 16 hold INF (callers), so row 0's minimum is the QP rows' minimum
+      const unsigned long long k = row_minkey(argkey(v, id));
+      const int kid = (int)(__builtin_amdgcn_readlane((int)(unsigned)k, 0) & 63);
+      const double w = bcast(v, kid >> shift);
+      if (w == INFINITY) {
+        v = INFINITY;
+        id = 0x7fffffff;
+      } else {
+        v = w;
+        id = kid;
+      }
+      return;
+    }
     row_argmin(v, id);
     v = bcast(v, 0);
     id = __builtin_amdgcn_readlane(id, 0);
