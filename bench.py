@@ -5,7 +5,8 @@ One step = score one batch of 4096 (N2=30, Nu=5, delta, lambda) candidates per G
 constrained closed loop + its GAM cost J1 per candidate (GAM_fun.m:81-111 per candidate), then
 one RCCL all-gather of the per-candidate costs and an identical stable ranking on every rank
 (SURVEY §8e).  Inputs are resident in HBM before the timed region.  Weak scaling: every rank
-scores its own contiguous 4096-candidate shard of a (4096 x world)-candidate grid.
+scores its own strided 4096-candidate shard (candidates rank, rank + world, ...) of a
+(4096 x world)-candidate grid.
 
 Launch:  python bench.py [--gpus 1 --steps K --warmup W]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -212,22 +213,22 @@ def main():
 
         tdist.init_process_group("nccl", device_id=dev)
 
-    from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_range
+    from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_indices
     from mpct.engine import eval_batch_device
     from mpct.scenarios import candidate_grid, shell3x3
 
     sc, r, yref = shell3x3(n2_max=args.n2, nu_max=args.nu)
     Cg = args.candidates * world
     N2, Nu, d, l = candidate_grid(Cg, N2=args.n2, Nu=args.nu)
-    lo, hi = shard_range(Cg, world, rank)
-    sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, lo, hi)
+    sidx = shard_indices(Cg, world, rank)
+    sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, sidx)
     # inputs resident in HBM before the timed region
     tN2 = torch.from_numpy(sN2).to(dev)
     tNu = torch.from_numpy(sNu).to(dev)
     td = torch.from_numpy(sd).to(dev)
     tl = torch.from_numpy(sl).to(dev)
     tr = torch.from_numpy(r[None].copy()).to(dev)
-    C = hi - lo
+    C = sidx.size
     out = dict(J1=torch.empty((C, sc.my), dtype=torch.float64, device=dev),
                j22=torch.empty((C, sc.my), dtype=torch.float64, device=dev),
                status=torch.empty(C, dtype=torch.int32, device=dev),
@@ -380,7 +381,7 @@ def main():
 def other_workload(args):
     """SURVEY §8d configs 3-5 through the same harness (barrier + synchronize around K timed steps,
     max over ranks, one JSON line on rank 0).  config 3 (shell7x5): the fixed 65,536-candidate
-    grid of tools/bench_config3.py split over the ranks (strong scaling, SURVEY: "65 536-candidate
+    grid of mpct.scenarios.config3_grid split over the ranks (strided) (strong scaling, SURVEY: "65 536-candidate
     grid sharded over 8xMI355X via RCCL"); config 5 (vandevusse): 4096 NMPC candidates per GPU;
     config 4 (dtc-mc): 10,000 candidates x 32 plant-mismatch draws split over the ranks.  One
     all-gather of the per-candidate cost records, identical ranking on every rank."""
@@ -394,18 +395,16 @@ def other_workload(args):
         import torch.distributed as tdist
 
         tdist.init_process_group("nccl", device_id=dev)
-    from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_range
+    from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_indices
     from mpct.engine import eval_batch_device
 
     v = None
     nref = 1
     if args.workload == "shell7x5":
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from bench_config3 import grid
-        from mpct.scenarios import SHELL7_W, shell7x5
+        from mpct.scenarios import SHELL7_W, config3_grid, shell7x5
 
         sc, r, vv, _ = shell7x5(n2_max=127, nu_max=15)
-        N2, Nu, d, l = grid(1024)
+        N2, Nu, d, l = config3_grid(1024)
         refs, v = r[None], vv[None]
         w = SHELL7_W
         scaling, metric = "strong", "closed-loop band-MPC sims/sec (Shell 7x5, 65,536-candidate grid)"
@@ -433,9 +432,9 @@ def other_workload(args):
         cfg = {"workload": "WoodBerry DTC-GPC Monte-Carlo, nit=200, sharded by candidate", "candidates": Cc,
                "draws": D}
     Cg = len(N2)
-    lo, hi = shard_range(Cg, world, rank)
-    sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, lo, hi)
-    C = hi - lo
+    sidx = shard_indices(Cg, world, rank)   # strided: every rank gets the same mix of (N2, Nu) cells
+    sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, sidx)
+    C = sidx.size
     S = C * nref
     t = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in
          dict(N2=sN2, Nu=sNu, d=sd, l=sl, r=refs).items()}

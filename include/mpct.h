@@ -31,8 +31,11 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 5 /* 5: one scenario on several GPUs of one process (mpct_eval_batch_multi,
-                              mpct_shard_range), kernel-instance query; the host-pointer entries wait on
+#define MPCT_ABI_VERSION 6 /* 6: strided multi-device shards (mpct_shard_candidates replaces the
+                              contiguous mpct_shard_range), a device may appear more than once in
+                              mpct_eval_batch_multi's list; dims table carries nit, nq.
+                              5: one scenario on several GPUs of one process (mpct_eval_batch_multi),
+                              kernel-instance query; the host-pointer entries wait on
                               their own stream only.  4: nonlinear MPC scenarios (mpct_nmpc_scenario_create); 3: MD feed-forward +
                               soft output bands; 2: DTC-GPC predictor + plant-only disturbances + plant
                               variants; v1..v3 descriptors accepted */
@@ -246,7 +249,7 @@ void mpct_scenario_destroy(mpct_scenario* s);
 
 /* Host-table inspection (testing / MATLAB-side debugging; no device needed).
  *   which: 0 = MV step table [my][nu][tlen], 1 = free-response table Phi [my*n2_max][nx],
- *          2 = dims {my, nu, nd, n2_max, nu_max, tlen, nx, nyh, nup},
+ *          2 = dims {my, nu, nd, n2_max, nu_max, tlen, nx, nyh, nup, nit, nq},
  *          3 = Phi on the device state basis [y-r, backward differences of y | du history]
  * Copies at most cap doubles into buf; returns the number of doubles the table holds, or <0. */
 int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, double* buf, int64_t cap);
@@ -275,21 +278,28 @@ int32_t mpct_eval_batch_device(mpct_scenario* s, int64_t C, const int32_t* N2, c
 
 /* Score C candidates on ndev GPUs of this process at once (host pointers, like mpct_eval_batch).
  * The candidates are independent (VNS2.m:148-169, GAM_fun.m:79-91 score each one in isolation),
- * so they are split into contiguous shards [k*ceil(C/ndev), (k+1)*ceil(C/ndev)) (mpct_shard_range),
- * shard k on devices[k]; each device gets its own copy of the scenario tables and its own stream,
- * one host thread per device drives its H2D copies, launch and D2H copies, and the call returns
+ * so they are split into strided shards: slot k scores candidates k, k+ndev, k+2*ndev, ...
+ * (mpct_shard_candidates) on devices[k].  Tuning grids are built cell by cell (all lambda draws of
+ * one (N2, Nu) pair together), so a contiguous split would hand one slot all the heavy horizons;
+ * the strided one gives every slot the same mix.  Each slot gets its own scenario context (a copy
+ * of the tables, its own stream and scratch), one host thread per slot gathers its candidates,
+ * drives the H2D copies, launch and D2H copies and scatters the results back, and the call returns
  * when every shard is done.  Results land in the caller's order (simulation s = c*nref + k), so a
- * single-threaded MATLAB host drives all GPUs of a node with one call.  ndev = 1 is exactly
- * mpct_eval_batch on devices[0].  opts->device is ignored.  Errors: the first failing device's
- * code, its message prefixed with "device <ordinal>: ". */
+ * single-threaded MATLAB host drives all GPUs of a node with one call.  A device ordinal may
+ * appear more than once (each occurrence gets its own context and stream on that device).
+ * ndev = 1 is exactly mpct_eval_batch on devices[0].  opts->device is ignored.  Every ordinal is
+ * checked before any work starts.  Errors: the first failing slot's code, its message prefixed
+ * with "device <ordinal>: ". */
 int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const int32_t* devices, int64_t C,
                               const int32_t* N2, const int32_t* Nu, const double* delta, const double* lambda,
                               int32_t nref, const double* r, const double* v, const mpct_opts* opts,
                               mpct_result* out);
 
-/* The contiguous shard [*lo, *hi) of C candidates that device slot k of ndev scores (the split of
- * mpct_eval_batch_multi and of the torch.distributed ranks).  Returns *hi - *lo, or <0. */
-int64_t mpct_shard_range(int64_t C, int32_t ndev, int32_t k, int64_t* lo, int64_t* hi);
+/* The strided shard of C candidates that device slot k of ndev scores (the split of
+ * mpct_eval_batch_multi and of the torch.distributed ranks, mpct.dist.shard_indices): candidates
+ * k, k+ndev, ... < C.  Writes at most cap indices into idx (idx may be NULL); returns the shard's
+ * size ceil((C - k) / ndev), or <0. */
+int64_t mpct_shard_candidates(int64_t C, int32_t ndev, int32_t k, int64_t* idx, int64_t cap);
 
 /* The ranking every rank computes after the cost all-gather (Shell3x3.m:161 ranks by
  * the Pareto-weighted cost): perm[0..C) = candidate indices by ascending s_c = sum_j costs[c*k+j] *

@@ -299,12 +299,13 @@ static void cmd_create_nmpc(mxArray* plhs[], const mxArray* d) {
 }
 
 /* the scenario's dimensions from the library (mpct_scenario_table which = 2) */
-static void dims_of(mpct_scenario* s, int* my, int* nu, int* nd) {
-  double dm[9];
-  if (mpct_scenario_table(s, 2, dm, 9) < 9) lib_error("mpct:eval");
+static void dims_of(mpct_scenario* s, int* my, int* nu, int* nv, int* nit) {
+  double dm[11];
+  if (mpct_scenario_table(s, 2, dm, 11) < 11) lib_error("mpct:eval");
   *my = (int)dm[0];
   *nu = (int)dm[1];
-  *nd = (int)dm[2];
+  *nv = (int)dm[2] + (int)dm[10]; /* v rows: measured + plant-only disturbances */
+  *nit = (int)dm[9];
 }
 
 static mpct_opts read_opts(const mxArray* o) {
@@ -344,23 +345,24 @@ static void cmd_eval(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[],
   if (nrhs < a0 + 5) mexErrMsgIdAndTxt("mpct:arg", "usage: mpct_mex('%s', h,%s N2, Nu, delta, lambda, r [, v, opts])",
                                        multi ? "eval_multi" : "eval", multi ? " devices," : "");
   mpct_scenario* s = handle(prhs[1]);
-  int my, nu, nd;
-  dims_of(s, &my, &nu, &nd);
+  int my, nu, nv, nit;
+  dims_of(s, &my, &nu, &nv, &nit);
   const long C = (long)mxGetNumberOfElements(prhs[a0]);
   int32_t* N2 = ints(prhs[a0], -1, "N2");
   int32_t* Nu = ints(prhs[a0 + 1], C, "Nu");
   double* delta = rows_of(prhs[a0 + 2], C, my, "delta");
   double* lambda = rows_of(prhs[a0 + 3], C, nu, "lambda");
-  const mxArray* ra = prhs[a0 + 4];
-  const mwSize* rd = mxGetDimensions(ra);
-  const int nit = mxGetNumberOfDimensions(ra) >= 2 ? (int)rd[1] : 0;
+  /* r and v are checked against the scenario's own my x nit and (nd + nq) x nit before anything
+   * is allocated: the library reads nref*my*nit and nref*(nd+nq)*nit doubles from them */
   int nref = 0;
-  double* r = signals(ra, my, nit, &nref, "r");
+  double* r = signals(prhs[a0 + 4], my, nit, &nref, "r");
   const mxArray* va = nrhs > a0 + 5 ? prhs[a0 + 5] : NULL;
   double* v = NULL;
-  if (va && !mxIsEmpty(va)) {
-    const int nv = (int)mxGetM(va);
-    v = signals(va, nv, nit, &nref, "v");
+  if (nv > 0) {
+    if (!va || mxIsEmpty(va)) mexErrMsgIdAndTxt("mpct:arg", "'v' must be %d x %d (x nref)", nv, nit);
+    v = signals(va, nv, nit, &nref, "v"); /* nv x nit, 1 or nref pages (broadcast) */
+  } else if (va && !mxIsEmpty(va)) {
+    mexErrMsgIdAndTxt("mpct:arg", "'v' given but the scenario has no disturbance inputs");
   }
   mpct_opts o = read_opts(nrhs > a0 + 6 ? prhs[a0 + 6] : NULL);
   int32_t* devs = NULL;
@@ -410,7 +412,6 @@ static void cmd_eval(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[],
     if (k < nout) plhs[k] = outs[k];
     else mxDestroyArray(outs[k]);
   }
-  (void)nd;
 }
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {

@@ -103,6 +103,9 @@ struct mpct_scenario {
   // device state, one context per device ordinal (created on first use, kept until destroy):
   // a scenario can be evaluated on several GPUs of one process (mpct_eval_batch_multi)
   std::vector<DevCtx*> ctx;
+  // further contexts of a device listed more than once in one mpct_eval_batch_multi call:
+  // extra[dev][j] serves its (j+2)-th occurrence (own stream, scratch and order buffers)
+  std::vector<std::vector<DevCtx*>> extra;
 };
 
 extern "C" int32_t mpct_abi_version(void) { return MPCT_ABI_VERSION; }
@@ -690,22 +693,27 @@ extern "C" int32_t mpct_nmpc_scenario_create(const mpct_nmpc_desc* d, mpct_scena
   return MPCT_OK;
 }
 
+static void ctx_release(DevCtx* c) {
+  (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->dtab) (void)hipFree(c->dtab);
+  if (c->dscratch) (void)hipFree(c->dscratch);
+  order_release(c->order);
+  c->fan.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
 extern "C" void mpct_scenario_destroy(mpct_scenario* s) {
   if (!s) return;
   int cur = -1;
-  const bool any = std::any_of(s->ctx.begin(), s->ctx.end(), [](DevCtx* c) { return c != nullptr; });
+  bool any = std::any_of(s->ctx.begin(), s->ctx.end(), [](DevCtx* c) { return c != nullptr; });
+  for (auto& v : s->extra) any = any || !v.empty();
   if (any && hipGetDevice(&cur) != hipSuccess) cur = -1;
-  for (DevCtx* c : s->ctx) {
-    if (!c) continue;
-    (void)hipSetDevice(c->dev);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->dtab) (void)hipFree(c->dtab);
-    if (c->dscratch) (void)hipFree(c->dscratch);
-    order_release(c->order);
-    c->fan.release();
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    delete c;
-  }
+  for (DevCtx* c : s->ctx)
+    if (c) ctx_release(c);
+  for (auto& v : s->extra)
+    for (DevCtx* c : v) ctx_release(c);
   if (cur >= 0) (void)hipSetDevice(cur);
   delete s;
 }
@@ -722,7 +730,7 @@ extern "C" int64_t mpct_scenario_table(const mpct_scenario* s, int32_t which, do
     src = &s->phid;
   else if (which == 2) {
     dims = {(double)s->my, (double)s->nu, (double)s->nd, (double)s->n2max, (double)s->numax,
-            (double)s->tlen, (double)s->nx, (double)s->nyh, (double)s->nup};
+            (double)s->tlen, (double)s->nx, (double)s->nyh, (double)s->nup, (double)s->nit, (double)s->nq};
     src = &dims;
   } else
     return fail(MPCT_EINVAL, "unknown table");
@@ -753,7 +761,10 @@ static void compact_taps(const mpct_scenario* s, DevScenario& ds) {
 
 // the context of device want_dev (-1: the calling thread's current device), created and its
 // tables uploaded on first use; makes that device current for the calling thread
-static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out) {
+static int build_ctx(mpct_scenario* s, int dev, DevCtx** out);
+
+// occurrence j of device want_dev in one call (0: the primary context; j >= 1: extra[dev][j-1])
+static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out, int occurrence = 0) {
   int dev = want_dev;
   if (dev < 0) {
     if (hipGetDevice(&dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
@@ -763,10 +774,25 @@ static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out) {
   if (dev >= cnt) return fail(MPCT_EINVAL, "device ordinal out of range");
   if (hipSetDevice(dev) != hipSuccess) return fail(MPCT_EDEVICE, "hipSetDevice failed");
   if ((int)s->ctx.size() < cnt) s->ctx.resize(cnt, nullptr);
-  if (s->ctx[dev]) {
-    *out = s->ctx[dev];
-    return MPCT_OK;
+  if ((int)s->extra.size() < cnt) s->extra.resize(cnt);
+  DevCtx** slot = nullptr;
+  if (occurrence == 0) {
+    slot = &s->ctx[dev];
+  } else {
+    auto& ex = s->extra[dev];
+    if ((int)ex.size() < occurrence) ex.resize(occurrence, nullptr);
+    slot = &ex[occurrence - 1];
   }
+  if (!*slot) {
+    const int rc = build_ctx(s, dev, slot);
+    if (rc) return rc;
+  }
+  *out = *slot;
+  return MPCT_OK;
+}
+
+// a new context on device dev (current): the scenario's tables uploaded, its own stream
+static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   // pack all tables into one allocation, 256-B aligned pieces
   std::vector<char> blob;
   auto put = [&](const void* p, size_t bytes) -> size_t {
@@ -876,7 +902,6 @@ static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out) {
   cx->dtab = dp;
   cx->dev = dev;
   if (!cx->fan.init(dev)) cx->fan.release();  // class launches over streams; no fan: one stream, still correct
-  s->ctx[dev] = cx;
   *out = cx;
   return MPCT_OK;
 }
@@ -1013,8 +1038,11 @@ static int eval_host(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* N2,
   };
   if (!h2d(o_N2, N2, C * 4) || !h2d(o_Nu, Nu, C * 4) || !h2d(o_d, delta, C * my * 8) ||
       !h2d(o_l, lambda, C * nu * 8) || !h2d(o_r, r, (size_t)nref * my * nit * 8) ||
-      (nd + s->nq > 0 && !h2d(o_v, v, (size_t)nref * (nd + s->nq) * nit * 8)))
+      (nd + s->nq > 0 && !h2d(o_v, v, (size_t)nref * (nd + s->nq) * nit * 8))) {
+    // copies enqueued before the failing one may still read the caller's buffers
+    (void)hipStreamSynchronize(st);
     return fail(MPCT_EDEVICE, "hipMemcpyAsync(inputs) failed");
+  }
   mpct_result dres{};
   dres.J1 = reinterpret_cast<double*>(b + o_J1);
   dres.j21 = reinterpret_cast<double*>(b + o_j21);
@@ -1067,18 +1095,29 @@ extern "C" int32_t mpct_eval_batch(mpct_scenario* s, int64_t C, const int32_t* N
   return eval_host(s, cx, C, N2, Nu, delta, lambda, nref, r, v, opts, out);
 }
 
-// result pointer of simulation s0 onwards (row-major per simulation), NULL stays NULL
-template <class T>
-static T* at(T* p, int64_t s0, int64_t width) {
-  return p ? p + s0 * width : nullptr;
+extern "C" int64_t mpct_shard_candidates(int64_t C, int32_t ndev, int32_t k, int64_t* idx, int64_t cap) {
+  if (C < 0 || ndev < 1 || k < 0 || k >= ndev) return fail(MPCT_EINVAL, "bad shard arguments");
+  const int64_t n = C > k ? (C - k + ndev - 1) / ndev : 0;
+  if (idx)
+    for (int64_t j = 0; j < std::min(n, cap); ++j) idx[j] = k + j * ndev;
+  return n;
 }
 
-extern "C" int64_t mpct_shard_range(int64_t C, int32_t ndev, int32_t k, int64_t* lo, int64_t* hi) {
-  if (C < 0 || ndev < 1 || k < 0 || k >= ndev || !lo || !hi) return fail(MPCT_EINVAL, "bad shard arguments");
-  const int64_t per = (C + ndev - 1) / ndev;
-  *lo = std::min<int64_t>(C, per * k);
-  *hi = std::min<int64_t>(C, per * (k + 1));
-  return *hi - *lo;
+// copy `width` elements per simulation between the caller's order and a shard's packed order:
+// simulation s = c*nref + q of candidate c = k + j*ndev <-> packed row j*nref + q
+template <class T>
+static void strided_copy(T* caller, T* packed, int64_t n, int32_t ndev, int32_t k, int32_t nref, int64_t width,
+                         bool to_caller) {
+  if (!caller || !packed) return;
+  for (int64_t j = 0; j < n; ++j) {
+    T* a = caller + (k + j * ndev) * (int64_t)nref * width;
+    T* b = packed + j * (int64_t)nref * width;
+    const size_t bytes = sizeof(T) * (size_t)nref * (size_t)width;
+    if (to_caller)
+      std::memcpy(a, b, bytes);
+    else
+      std::memcpy(b, a, bytes);
+  }
 }
 
 extern "C" int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const int32_t* devices, int64_t C,
@@ -1090,43 +1129,80 @@ extern "C" int32_t mpct_eval_batch_multi(mpct_scenario* s, int32_t ndev, const i
   if (!out) return fail(MPCT_EINVAL, "null result");
   if (ndev < 1 || ndev > 64 || !devices) return fail(MPCT_EINVAL, "ndev must be 1..64 with a device list");
   if (s->dtc && opts && opts->open_loop) return fail(MPCT_EINVAL, "DTC mode has no open-loop prediction");
-  for (int a = 0; a < ndev; ++a)
-    for (int b2 = a + 1; b2 < ndev; ++b2)
-      if (devices[a] == devices[b2]) return fail(MPCT_EINVAL, "duplicate device in the list");
-  int cur = -1;
-  if (hipGetDevice(&cur) != hipSuccess) return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
-  // contexts (table uploads) serially on this thread, before any worker starts
+  int cur = -1, cnt = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0)
+    return fail(MPCT_EDEVICE, "hipGetDevice failed (no GPU?)");
+  // every ordinal is checked before any context exists or any device is made current
+  for (int k = 0; k < ndev; ++k)
+    if (devices[k] < 0 || devices[k] >= cnt) return fail(MPCT_EINVAL, "device ordinal out of range");
+  // contexts (table uploads) serially on this thread, before any worker starts; a device listed
+  // again gets a further context of its own
   std::vector<DevCtx*> cxs(ndev, nullptr);
   for (int k = 0; k < ndev; ++k) {
-    if (devices[k] < 0) return fail(MPCT_EINVAL, "device ordinals must be >= 0");
-    rc = device_ctx(s, devices[k], &cxs[k]);
+    int occ = 0;
+    for (int j = 0; j < k; ++j) occ += devices[j] == devices[k];
+    rc = device_ctx(s, devices[k], &cxs[k], occ);
     if (rc) {
       (void)hipSetDevice(cur);
       return rc;
     }
   }
-  const int my = s->my, nu = s->nu, nin = s->nd + s->nq, nit = s->nit;
-  (void)nin;
+  const int my = s->my, nu = s->nu, nit = s->nit;
   std::vector<int> rcs(ndev, MPCT_OK);
   std::vector<std::string> errs(ndev);
   auto shard = [&](int k) {
-    int64_t lo = 0, hi = 0;
-    mpct_shard_range(C, ndev, k, &lo, &hi);
-    if (hi <= lo) return;
-    const int64_t s0 = lo * nref;  // simulations of candidate lo onwards (s = c*nref + kref)
+    const int64_t n = mpct_shard_candidates(C, ndev, k, nullptr, 0);
+    if (n <= 0) {
+      rcs[k] = hipSetDevice(cxs[k]->dev) == hipSuccess ? MPCT_OK : MPCT_EDEVICE;
+      return;
+    }
+    if (ndev == 1) {  // the identity split: no gather / scatter
+      rcs[k] = eval_host(s, cxs[k], C, N2, Nu, delta, lambda, nref, r, v, opts, out);
+      if (rcs[k]) errs[k] = g_err;
+      return;
+    }
+    // gather this slot's candidates (k, k+ndev, ...) and give it packed result buffers
+    std::vector<int32_t> n2(n), nuv(n);
+    std::vector<double> dl((size_t)n * my), lm((size_t)n * nu);
+    strided_copy(const_cast<int32_t*>(N2), n2.data(), n, ndev, k, 1, 1, false);
+    strided_copy(const_cast<int32_t*>(Nu), nuv.data(), n, ndev, k, 1, 1, false);
+    strided_copy(const_cast<double*>(delta), dl.data(), n, ndev, k, 1, my, false);
+    strided_copy(const_cast<double*>(lambda), lm.data(), n, ndev, k, 1, nu, false);
+    const int64_t S = n * nref;
+    auto buf = [&](const void* want, int64_t w) { return want ? std::vector<double>((size_t)(S * w)) : std::vector<double>(); };
+    std::vector<double> J1 = buf(out->J1, my), j21 = buf(out->j21, my), j22 = buf(out->j22, my), Jnu = buf(out->Jnu, nu);
+    std::vector<double> y = buf(out->y, (int64_t)my * nit), u = buf(out->u, (int64_t)nu * nit);
+    std::vector<double> ys = buf(out->ys, (int64_t)my * nit), uo = buf(out->uopt, (int64_t)nu * nit);
+    std::vector<int32_t> stv(out->status ? (size_t)S : 0);
+    std::vector<int64_t> itv(out->qp_iters ? (size_t)S : 0);
+    auto p = [](std::vector<double>& x) { return x.empty() ? nullptr : x.data(); };
     mpct_result o{};
-    o.J1 = at(out->J1, s0, my);
-    o.j21 = at(out->j21, s0, my);
-    o.j22 = at(out->j22, s0, my);
-    o.Jnu = at(out->Jnu, s0, nu);
-    o.status = at(out->status, s0, 1);
-    o.qp_iters = at(out->qp_iters, s0, 1);
-    o.y = at(out->y, s0, (int64_t)my * nit);
-    o.u = at(out->u, s0, (int64_t)nu * nit);
-    o.ys = at(out->ys, s0, (int64_t)my * nit);
-    o.uopt = at(out->uopt, s0, (int64_t)nu * nit);
-    rcs[k] = eval_host(s, cxs[k], hi - lo, N2 + lo, Nu + lo, delta + lo * my, lambda + lo * nu, nref, r, v, opts, &o);
-    if (rcs[k]) errs[k] = g_err;  // g_err is thread-local: carry it to the caller
+    o.J1 = p(J1);
+    o.j21 = p(j21);
+    o.j22 = p(j22);
+    o.Jnu = p(Jnu);
+    o.status = stv.empty() ? nullptr : stv.data();
+    o.qp_iters = itv.empty() ? nullptr : itv.data();
+    o.y = p(y);
+    o.u = p(u);
+    o.ys = p(ys);
+    o.uopt = p(uo);
+    rcs[k] = eval_host(s, cxs[k], n, n2.data(), nuv.data(), dl.data(), lm.data(), nref, r, v, opts, &o);
+    if (rcs[k]) {
+      errs[k] = g_err;  // g_err is thread-local: carry it to the caller
+      return;
+    }
+    // scatter into the caller's order (slots write disjoint candidates)
+    strided_copy(out->J1, o.J1, n, ndev, k, nref, my, true);
+    strided_copy(out->j21, o.j21, n, ndev, k, nref, my, true);
+    strided_copy(out->j22, o.j22, n, ndev, k, nref, my, true);
+    strided_copy(out->Jnu, o.Jnu, n, ndev, k, nref, nu, true);
+    strided_copy(out->status, o.status, n, ndev, k, nref, 1, true);
+    strided_copy(out->qp_iters, o.qp_iters, n, ndev, k, nref, 1, true);
+    strided_copy(out->y, o.y, n, ndev, k, nref, (int64_t)my * nit, true);
+    strided_copy(out->u, o.u, n, ndev, k, nref, (int64_t)nu * nit, true);
+    strided_copy(out->ys, o.ys, n, ndev, k, nref, (int64_t)my * nit, true);
+    strided_copy(out->uopt, o.uopt, n, ndev, k, nref, (int64_t)nu * nit, true);
   };
   if (ndev == 1) {
     shard(0);

@@ -84,11 +84,11 @@ class MpctResult(C.Structure):
 EXPORTS = [
     "mpct_abi_version", "mpct_last_error", "mpct_scenario_create", "mpct_scenario_destroy",
     "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
-    "mpct_nmpc_scenario_create", "mpct_eval_batch_multi", "mpct_shard_range", "mpct_kernel_instance",
+    "mpct_nmpc_scenario_create", "mpct_eval_batch_multi", "mpct_shard_candidates", "mpct_kernel_instance",
     "mpct_rank_device",
 ]
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 ST_QP_MAXITER, ST_QP_INFEAS, ST_NONFINITE, ST_SKIPPED, ST_BADHORIZON = 1, 2, 4, 8, 16
 ST_SQP_MAXITER, ST_BOUNDS = 32, 64
 NMPC_VANDEVUSSE = 1
@@ -141,8 +141,8 @@ def load():
     lib.mpct_lds_bytes.restype = C.c_int64
     lib.mpct_eval_batch_multi.argtypes = [C.c_void_p, C.c_int32, c_int32_p] + batch_args[1:]
     lib.mpct_eval_batch_multi.restype = C.c_int32
-    lib.mpct_shard_range.argtypes = [C.c_int64, C.c_int32, C.c_int32, c_int64_p, c_int64_p]
-    lib.mpct_shard_range.restype = C.c_int64
+    lib.mpct_shard_candidates.argtypes = [C.c_int64, C.c_int32, C.c_int32, c_int64_p, C.c_int64]
+    lib.mpct_shard_candidates.restype = C.c_int64
     lib.mpct_kernel_instance.argtypes = [C.c_void_p, C.POINTER(MpctOpts), C.c_char_p, C.c_int32]
     lib.mpct_kernel_instance.restype = C.c_int32
     lib.mpct_rank_device.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]

@@ -1,5 +1,10 @@
-"""Candidate-level data parallelism: one process per GPU, contiguous candidate
-shards, one all-gather of the per-candidate cost records, identical ranking on every rank.
+"""Candidate-level data parallelism: one process per GPU, strided candidate shards,
+one all-gather of the per-candidate cost records, identical ranking on every rank.
+
+Rank r of W scores candidates r, r+W, r+2W, ... (the split of mpct_eval_batch_multi /
+mpct_shard_candidates).  The tuning grids are built cell by cell (config 3: all 1024 lambda draws
+of one (N2, Nu) pair together, N2-major), so a contiguous split hands rank r one horizon and the
+heaviest rank sets the time; the strided split gives every rank the same mix of cells.
 
 Nothing is exchanged during a simulation (VNS2.m:148-169 and GAM_fun.m:79-91 evaluate every
 candidate in isolation), so the only collective is the final all-gather.  The functions here are
@@ -13,37 +18,41 @@ import torch
 SKIPPED_N2 = 0  # sentinel candidate: the kernel returns status MPCT_ST_SKIPPED (8) and NaN costs
 
 
-def shard_range(C: int, world: int, rank: int):
-    """[lo, hi) of rank's contiguous shard of a C-candidate grid padded to a multiple of world
-    (per = ceil(C / world)); hi may exceed C — those slots are sentinel padding."""
+def shard_indices(C: int, world: int, rank: int) -> np.ndarray:
+    """Candidates of rank's strided shard of a C-candidate grid padded to a multiple of world:
+    rank, rank + world, ... (ceil(C / world) of them); indices >= C are sentinel padding."""
     per = -(-C // world)
-    return rank * per, (rank + 1) * per
+    return rank + world * np.arange(per, dtype=np.int64)
 
 
-def pad_shard(N2, Nu, delta, lam, lo: int, hi: int):
-    """Slice [lo, hi) of the candidate arrays, padding past the end with skipped sentinels."""
+def pad_shard(N2, Nu, delta, lam, idx):
+    """The candidate arrays at ``idx`` (shard_indices), padding indices >= C with skipped
+    sentinels (N2 = 0: status 8, NaN costs)."""
     C = len(N2)
-    n = hi - lo
-    take = max(0, min(hi, C) - lo)
+    idx = np.asarray(idx, dtype=np.int64)
+    live = idx < C
+    n = idx.size
     my, nu = delta.shape[1], lam.shape[1]
     oN2 = np.full(n, SKIPPED_N2, dtype=np.int32)
     oNu = np.ones(n, dtype=np.int32)
     od = np.ones((n, my))
     ol = np.ones((n, nu))
-    oN2[:take], oNu[:take] = N2[lo:lo + take], Nu[lo:lo + take]
-    od[:take], ol[:take] = delta[lo:lo + take], lam[lo:lo + take]
+    oN2[live], oNu[live] = N2[idx[live]], Nu[idx[live]]
+    od[live], ol[live] = delta[idx[live]], lam[idx[live]]
     return oN2, oNu, od, ol
 
 
 def gather_costs(local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather equal-size per-rank cost records [n, K] -> [world * n, K] in rank order."""
+    """All-gather equal-size per-rank cost records [n, K] of the strided shards -> [world * n, K]
+    in candidate order: the gathered block is rank-major, row j of rank r is candidate r + j*world,
+    so one transpose of the (world, n) leading axes restores the grid's order."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
+    n = local.shape[0]
+    out = torch.empty((world * n,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    return out
+    return out.view((world, n) + tuple(local.shape[1:])).transpose(0, 1).reshape((world * n,) + tuple(local.shape[1:]))
 
 
 def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = None) -> torch.Tensor:

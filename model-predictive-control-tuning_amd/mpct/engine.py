@@ -315,18 +315,22 @@ def kernel_instance(sc: Scenario, open_loop=False, want_traj=False) -> str:
     return buf.value.decode()
 
 
-def shard_range(C_: int, ndev: int, k: int):
-    """mpct_shard_range: the contiguous candidate shard [lo, hi) of device slot k."""
-    lo, hi = C.c_int64(), C.c_int64()
-    if _lib.load().mpct_shard_range(int(C_), int(ndev), int(k), C.byref(lo), C.byref(hi)) < 0:
+def shard_candidates(C_: int, ndev: int, k: int) -> np.ndarray:
+    """mpct_shard_candidates: the candidates of device slot k (k, k+ndev, ... < C)."""
+    lib = _lib.load()
+    n = lib.mpct_shard_candidates(int(C_), int(ndev), int(k), None, 0)
+    if n < 0:
         raise MpctError(_lib.last_error())
-    return lo.value, hi.value
+    idx = np.zeros(n, dtype=np.int64)
+    lib.mpct_shard_candidates(int(C_), int(ndev), int(k), idx.ctypes.data_as(_lib.c_int64_p), n)
+    return idx
 
 
 def eval_batch_multi(sc: Scenario, devices, N2, Nu, delta, lam, refs, v=None, open_loop=False,
                      want_traj=False, max_qp_iter=0, feas_tol=0.0) -> EvalResult:
     """mpct_eval_batch_multi: one call scores the candidates on every GPU of ``devices`` at once
-    (contiguous shards, one host thread and stream per device, results in the caller's order)."""
+    (strided shards, one host thread, context and stream per list entry, results in the caller's
+    order; a device may be listed more than once)."""
     devs = np.ascontiguousarray(np.atleast_1d(devices), dtype=np.int32)
     N2 = np.ascontiguousarray(np.atleast_1d(N2), dtype=np.int32)
     Cn = N2.size

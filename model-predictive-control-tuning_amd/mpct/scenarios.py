@@ -111,6 +111,26 @@ SHELL7_TUNED = dict(N=27, Nu=(2, 2, 2), delta=(0.0,) * 7,
 SHELL7_W = np.array([1e-4, 1e-4, 1, 0.5, 1, 0.5, 1])               # Shell7x5.m:202 (GAM weights)
 
 
+CONFIG3_N2 = (16, 24, 32, 48, 64, 96, 112, 127)
+CONFIG3_NU = (2, 3, 4, 6, 8, 10, 12, 15)
+
+
+def config3_grid(per=1024, seed=20250307):
+    """BASELINE config 3 grid: N2 x Nu cells (N2-major, 64 cells) x ``per``
+    lambda draws log10 U(-3, 1) (numpy default_rng(seed)), delta = 0 (band mode, Shell7x5.m:190).
+    Candidate c sits in cell c // per: N2 = CONFIG3_N2[cell // 8], Nu = CONFIG3_NU[cell % 8]."""
+    rng = np.random.default_rng(seed)
+    N2 = np.repeat(np.array([n for n in CONFIG3_N2 for _ in CONFIG3_NU], np.int32), per)
+    Nu = np.repeat(np.array([u for _ in CONFIG3_N2 for u in CONFIG3_NU], np.int32), per)
+    lam = 10.0 ** rng.uniform(-3, 1, size=(N2.size, 3))
+    return N2, Nu, np.zeros((N2.size, 7)), lam
+
+
+def config3_stratified(per_cell=128, per=1024):
+    """Indices of the first ``per_cell`` lambda draws of every config-3 cell (the parity sample)."""
+    return (np.arange(64)[:, None] * per + np.arange(per_cell)[None, :]).ravel()
+
+
 def shell7x5_plant(L=SHELL7_L, R=SHELL7_R):
     """Pze = L * c2d([Gs Ds], Ts, 'zoh') * R  (Shell7x5.m:93-98, MPCTuning.m:162)."""
     return [[c2d([SHELL7_K[i, j]], [SHELL7_TAU[i, j], 1.0], SHELL7_TS, SHELL7_DELAY[i, j]).scale(L[i] * R[j])

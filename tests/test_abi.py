@@ -35,7 +35,7 @@ def test_header_and_exports_agree(built):
 def test_abi_version(built):
     from mpct import _lib
 
-    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_abi_v1_descriptor_accepted(built, monkeypatch):
@@ -227,26 +227,22 @@ def test_kernel_isa_invariants(built):
     assert 12 * sc.lds_bytes(30, 5) <= 160 * 1024
 
 
-def test_shard_range_matches_dist(built):
-    """mpct_shard_range (the split of mpct_eval_batch_multi) equals the torch.distributed ranks'
-    split (mpct.dist.shard_range): contiguous, covering, ceil(C/W) per slot."""
-    from mpct.dist import shard_range as dist_range
-    from mpct.engine import shard_range
+def test_shard_candidates_strided(built):
+    """mpct_shard_candidates (the split of mpct_eval_batch_multi): slot k gets k, k+W, ... < C,
+    ceil((C-k)/W) of them, capped writes; bad arguments fail."""
+    from mpct import _lib
+    from mpct.engine import shard_candidates
 
     for C_, W in [(0, 1), (1, 8), (7, 8), (4096, 1), (4096, 3), (65536, 8), (10000, 7)]:
-        got = [shard_range(C_, W, k) for k in range(W)]
-        # the ranks pad their last shard with sentinels; the in-process split clips at C
-        assert got == [tuple(min(x, C_) for x in dist_range(C_, W, k)) for k in range(W)]
-        assert got[0][0] == 0 and got[-1][1] == C_
-        assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
-        per = -(-C_ // W)
-        assert all(hi - lo <= per for lo, hi in got)
-    from mpct import _lib
-
-    lo, hi = C.c_int64(), C.c_int64()
-    assert _lib.load().mpct_shard_range(10, 0, 0, C.byref(lo), C.byref(hi)) < 0
-    assert _lib.load().mpct_shard_range(10, 2, 2, C.byref(lo), C.byref(hi)) < 0
-
+        got = [shard_candidates(C_, W, k) for k in range(W)]
+        np.testing.assert_array_equal(np.sort(np.concatenate(got)), np.arange(C_))
+        for k, g in enumerate(got):
+            np.testing.assert_array_equal(g, np.arange(k, C_, W))
+    lib = _lib.load()
+    buf = (C.c_int64 * 2)()
+    assert lib.mpct_shard_candidates(10, 3, 1, buf, 2) == 3 and list(buf) == [1, 4]
+    assert lib.mpct_shard_candidates(10, 0, 0, None, 0) < 0
+    assert lib.mpct_shard_candidates(10, 2, 2, None, 0) < 0
 
 def test_kernel_instance_and_multi_validation(built):
     """The instance query needs no device; mpct_eval_batch_multi validates before touching one."""
@@ -265,8 +261,10 @@ def test_kernel_instance_and_multi_validation(built):
                                                      "<64,false,true>")
     N2 = np.full(4, 30, np.int32)
     d = np.full((4, 3), 0.1)
-    with pytest.raises(MpctError, match="duplicate"):
-        eval_batch_multi(sc, [0, 0], N2, 5, d, d, r[None])
+    # ordinals are checked before any context is built or device made current (a device may be
+    # listed more than once: each occurrence gets its own context, tests/test_gpu_parity.py)
+    with pytest.raises(MpctError, match="no GPU|out of range"):
+        eval_batch_multi(sc, [0, -1], N2, 5, d, d, r[None])
     with pytest.raises(MpctError, match="ndev"):
         eval_batch_multi(sc, [], N2, 5, d, d, r[None])
     lib = _lib.load()

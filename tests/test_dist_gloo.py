@@ -1,5 +1,5 @@
-"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py — contiguous
-candidate shards with sentinel padding, one all-gather of the per-candidate cost records, and an
+"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py — strided
+candidate shards (rank r scores r, r + W, ...) with sentinel padding, one all-gather of the per-candidate cost records, and an
 identical ranking on every rank that equals the single-process ranking.  Per-candidate costs come
 from the C port (oracle/cgpc.c) here, standing in for the kernel, which needs a GPU."""
 import os
@@ -38,12 +38,11 @@ def _worker(rank, world, port, C, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_range
+        from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_indices
         from mpct.scenarios import candidate_grid
 
         N2, Nu, d, l = candidate_grid(C)
-        lo, hi = shard_range(C, world, rank)
-        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, lo, hi)
+        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, shard_indices(C, world, rank))
         local = torch.from_numpy(_costs(sN2, sNu, sd, sl))
         g = gather_costs(local)
         w = torch.tensor([0.05, 0.40, 0.55], dtype=torch.float64)
@@ -82,11 +81,35 @@ def test_two_rank_gather_and_rank(built, C):
     np.testing.assert_array_equal(got[0][2], got[1][2])
 
 
-def test_shard_range_covers_grid():
-    from mpct.dist import shard_range
+def test_shard_indices_cover_grid_and_match_library(built):
+    """The ranks' strided split (mpct.dist.shard_indices) covers every candidate exactly once, pads
+    fewer than W sentinels, and equals the library's split of mpct_eval_batch_multi
+    (mpct_shard_candidates) on the real candidates."""
+    from mpct.dist import shard_indices
+    from mpct.engine import shard_candidates
 
     for C in (1, 7, 4096, 65536):
         for W in (1, 2, 3, 8):
-            spans = [shard_range(C, W, r) for r in range(W)]
-            assert spans[0][0] == 0 and all(spans[i][1] == spans[i + 1][0] for i in range(W - 1))
-            assert spans[-1][1] >= C and spans[-1][1] - C < W
+            parts = [shard_indices(C, W, r) for r in range(W)]
+            allc = np.sort(np.concatenate(parts))
+            np.testing.assert_array_equal(allc[:C], np.arange(C))
+            assert allc.size - C < W and np.all(allc[C:] >= C)
+            for r in range(W):
+                np.testing.assert_array_equal(shard_candidates(C, W, r), parts[r][parts[r] < C])
+
+
+def test_config3_strided_shards_are_balanced():
+    """Config 3's grid is cell-ordered (1024 lambda draws per (N2, Nu) cell, N2-major): the
+    contiguous split of round 2 gave rank r of 8 exactly N2 = CONFIG3_N2[r]; the strided split gives
+    every rank 128 draws of every cell, so the per-rank work model (sum of N2 * (3 Nu + 1) over the
+    shard, the output-row scan of DESIGN §7) is equal on every rank."""
+    from mpct.dist import shard_indices
+    from mpct.scenarios import config3_grid
+
+    N2, Nu, D, L = config3_grid(1024)
+    work = N2.astype(float) * (3 * Nu + 1)
+    for W in (2, 4, 8):
+        per_rank = [work[shard_indices(N2.size, W, r)].sum() for r in range(W)]
+        assert max(per_rank) / np.mean(per_rank) == 1.0
+        contiguous = [work[r * N2.size // W:(r + 1) * N2.size // W].sum() for r in range(W)]
+        assert max(contiguous) / np.mean(contiguous) > 1.3

@@ -363,8 +363,10 @@ def test_metric_instance_numpy_oracle_sample(metric):
 
 
 def test_multi_device_entry_equals_single(metric):
-    """mpct_eval_batch_multi on the devices this box has: bitwise equal to mpct_eval_batch
-    (ndev = 1 here; with more GPUs every shard runs the same kernel on its own device)."""
+    """mpct_eval_batch_multi, bitwise equal to mpct_eval_batch: on the box's devices, and with the
+    threaded strided path exercised on one GPU by listing device 0 twice and three times (each
+    occurrence is its own context, stream and host thread).  Results land in
+    the caller's order whatever the split."""
     import torch
 
     from mpct.engine import eval_batch, eval_batch_multi
@@ -373,13 +375,17 @@ def test_multi_device_entry_equals_single(metric):
     N2, Nu, d, l = candidate_grid(1000)
     devs = list(range(torch.cuda.device_count()))
     a = eval_batch(metric["sc"], N2, Nu, d, l, metric["r"][None], device=0)
-    b = eval_batch_multi(metric["sc"], devs, N2, Nu, d, l, metric["r"][None])
-    assert np.array_equal(a.J1, b.J1) and np.array_equal(a.status, b.status)
-    assert np.array_equal(a.qp_iters, b.qp_iters)
-    # open-loop + trajectories through the same entry (every result array is sharded)
-    c = eval_batch(metric["sc"], N2[:8], Nu[:8], d[:8], l[:8], metric["r"][None], open_loop=True,
-                   want_traj=True, device=0)
-    e = eval_batch_multi(metric["sc"], devs, N2[:8], Nu[:8], d[:8], l[:8], metric["r"][None], open_loop=True,
-                         want_traj=True)
-    for k in ("J1", "j21", "j22", "Jnu", "y", "u", "ys", "uopt"):
-        assert np.array_equal(getattr(c, k), getattr(e, k)), k
+    for dl in (devs, [0, 0], [0, 0, 0]):
+        b = eval_batch_multi(metric["sc"], dl, N2, Nu, d, l, metric["r"][None])
+        assert np.array_equal(a.J1, b.J1) and np.array_equal(a.status, b.status), dl
+        assert np.array_equal(a.qp_iters, b.qp_iters), dl
+    # open-loop + trajectories and two reference sets through the same entry (every result array
+    # is gathered and scattered, simulation s = c*nref + k)
+    from mpct.scenarios import vns_step_refs
+
+    refs = vns_step_refs(3, 500)[:2]
+    c = eval_batch(metric["sc"], N2[:9], Nu[:9], d[:9], l[:9], refs, open_loop=True, want_traj=True, device=0)
+    for dl in (devs, [0, 0]):
+        e = eval_batch_multi(metric["sc"], dl, N2[:9], Nu[:9], d[:9], l[:9], refs, open_loop=True, want_traj=True)
+        for k in ("J1", "j21", "j22", "Jnu", "status", "qp_iters", "y", "u", "ys", "uopt"):
+            assert np.array_equal(getattr(c, k), getattr(e, k)), (dl, k)

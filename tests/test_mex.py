@@ -148,7 +148,23 @@ def test_mex_library_errors_surface(built, has_gpu):
                (1, ["eval", ("P", 0, 0), [30, 30], [5, 5], np.ones((3, 3)), np.ones((2, 3)), r]),
                (1, ["eval", ("P", 0, 0), [30], [5], np.ones((1, 3)), np.ones((1, 3)), r[:, :10]])])
     assert res[1] == (False, ("mpct:arg", "'delta' must be 2 x 3 (one candidate per row)"))
-    assert not res[2][0]
+    # r / v are checked against the scenario's own nit and nd + nq: a short r or a v
+    # with too few rows would make the library read past the caller's buffers
+    assert res[2] == (False, ("mpct:arg", "'r' must be 3 x 500 (x nref)"))
+    _, r7, v7, d7 = shell7x5_desc()
+    lam = np.ones((1, 3))
+    res = mex([(1, ["create", d7]),
+               (1, ["eval", ("P", 0, 0), [16], [2], np.zeros((1, 7)), lam, r7, v7[:1]]),
+               (1, ["eval", ("P", 0, 0), [16], [2], np.zeros((1, 7)), lam, r7]),
+               (1, ["eval", ("P", 0, 0), [16], [2], np.zeros((1, 7)), lam, r7, v7[:, :50]]),
+               (1, ["eval", ("P", 0, 0), [16], [2], np.zeros((1, 7)), lam, r7[:, :199], v7])])
+    assert res[1] == (False, ("mpct:arg", "'v' must be 2 x 200 (x nref)"))
+    assert res[2] == (False, ("mpct:arg", "'v' must be 2 x 200 (x nref)"))
+    assert res[3] == (False, ("mpct:arg", "'v' must be 2 x 200 (x nref)"))
+    assert res[4] == (False, ("mpct:arg", "'r' must be 7 x 200 (x nref)"))
+    res = mex([(1, ["create", d]),
+               (1, ["eval", ("P", 0, 0), [30], [5], np.ones((1, 3)), np.ones((1, 3)), r, np.ones((1, 500))])])
+    assert res[1] == (False, ("mpct:arg", "'v' given but the scenario has no disturbance inputs"))
     if not has_gpu:
         res = mex([(1, ["create", d]), (1, ["eval", ("P", 0, 0), [30], [5], np.ones((1, 3)), np.ones((1, 3)), r])])
         assert not res[1][0] and res[1][1][0] == "mpct:eval"

@@ -17,16 +17,7 @@ import torch  # noqa: E402
 from mpct.engine import eval_batch_device  # noqa: E402
 from mpct.scenarios import SHELL7_W, shell7x5  # noqa: E402
 
-N2S = (16, 24, 32, 48, 64, 96, 112, 127)
-NUS = (2, 3, 4, 6, 8, 10, 12, 15)
-
-
-def grid(per=1024, seed=20250307):
-    rng = np.random.default_rng(seed)
-    N2 = np.repeat(np.array([n for n in N2S for _ in NUS], np.int32), per)
-    Nu = np.repeat(np.array([u for _ in N2S for u in NUS], np.int32), per)
-    lam = 10.0 ** rng.uniform(-3, 1, size=(N2.size, 3))
-    return N2, Nu, np.zeros((N2.size, 7)), lam
+from mpct.scenarios import config3_grid as grid  # noqa: E402,F401  (the grid lives in the product)
 
 
 def main():

@@ -1,0 +1,97 @@
+"""Config-3 cost parity report: the mdband kernel over the whole 65,536
+grid against the C restatement's fixture (tests/golden/config3_cband.npz, oracle/cband.c).
+
+Writes a JSON report: the fraction of candidates whose J1 (stratified 8,192, per output) or F =
+J1 @ SHELL7_W (whole grid) differs by more than 1e-6 relative, the top-64 ranking check, and for
+the divergent candidates of the sample: the per-step replay (oracle first move at the state the
+device reached, all 200 steps) and the first step at which the device's free run leaves the
+C port's free run.  Usage: python tools/config3_parity.py --out profiles/r03_config3_parity.json"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "model-predictive-control-tuning_amd")]
+
+from mpct.engine import eval_batch  # noqa: E402
+from mpct.scenarios import SHELL7_W, config3_grid, config3_stratified, shell7x5  # noqa: E402
+from oracle.cband import CBand  # noqa: E402
+from oracle.scenarios import shell7x5 as o_shell7x5  # noqa: E402
+
+FIXTURE = os.path.join(ROOT, "tests", "golden", "config3_cband.npz")
+
+
+def compare(threads=16, nrep=48):
+    d = np.load(FIXTURE)
+    sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
+    N2, Nu, D, L = config3_grid(1024)
+    t0 = time.time()
+    res = eval_batch(sc, N2, Nu, D, L, r[None], v=v[None])
+    t_gpu = time.time() - t0
+    F = res.J1 @ SHELL7_W
+    relF = np.abs(F - d["F_full"]) / np.abs(d["F_full"])
+    s = config3_stratified(128)
+    J = res.J1[s]
+    relJ = np.max(np.abs(J - d["J1_strat"]) / np.maximum(np.abs(d["J1_strat"]), 1e-300), axis=1)
+    top_g = np.argsort(F, kind="stable")[:64]
+    top_o = np.argsort(d["F_full"], kind="stable")[:64]
+    rep = dict(candidates=int(N2.size), gpu_status_nonzero=int(np.sum(res.status != 0)),
+               oracle_status_nonzero=int(np.sum(d["st_full"] != 0)), gpu_host_call_s=t_gpu,
+               F_frac_gt_1e6=float(np.mean(relF > 1e-6)), F_n_gt_1e6=int(np.sum(relF > 1e-6)),
+               F_median_rel=float(np.median(relF)), F_max_rel=float(relF.max()),
+               J1_strat_frac_gt_1e6=float(np.mean(relJ > 1e-6)), J1_strat_n_gt_1e6=int(np.sum(relJ > 1e-6)),
+               J1_strat_median_rel=float(np.median(relJ)), J1_strat_max_rel=float(relJ.max()),
+               top64_identical=bool(np.array_equal(top_g, top_o)),
+               top64_set_identical=bool(set(top_g.tolist()) == set(top_o.tolist())),
+               top64_max_rel=float(relF[top_o].max()),
+               top64_cells=sorted({(int(N2[c]), int(Nu[c])) for c in top_o}))
+    # divergence by cell (N2, Nu)
+    cells = {}
+    for c in np.nonzero(relF > 1e-6)[0]:
+        k = "%d/%d" % (N2[c], Nu[c])
+        cells[k] = cells.get(k, 0) + 1
+    rep["F_gt_1e6_by_cell"] = dict(sorted(cells.items(), key=lambda kv: -kv[1]))
+    # replay of divergent sample candidates
+    div = s[relJ > 1e-6]
+    pick = div[np.linspace(0, div.size - 1, min(nrep, div.size)).astype(int)] if div.size else div
+    rep["replay"] = []
+    if pick.size:
+        osc, orr, ov, oyref, fx = o_shell7x5()
+        cb = CBand(osc, 200, oyref)
+        g = eval_batch(sc, N2[pick], Nu[pick], D[pick], L[pick], r[None], v=v[None], want_traj=True)
+        du_o, du_a, st = cb.replay(N2[pick], Nu[pick], D[pick], L[pick], orr, ov, g.u, T=200, threads=threads)
+        o = cb.eval(N2[pick], Nu[pick], D[pick], L[pick], orr[None], ov[None], want_traj=True, threads=threads)
+        for k, c in enumerate(pick):
+            scale = max(float(np.abs(du_o[k]).max()), 1e-300)
+            err = np.abs(du_a[k] - du_o[k]).max(axis=0) / scale
+            diff_u = np.abs(g.u[k] - o["u"][k]).max(axis=0) / max(float(np.abs(o["u"][k]).max()), 1e-300)
+            first = int(np.argmax(diff_u > 1e-9)) if np.any(diff_u > 1e-9) else -1
+            rep["replay"].append(dict(
+                cand=int(c), N2=int(N2[c]), Nu=int(Nu[c]), lam=L[c].tolist(),
+                J1_rel=float(np.max(np.abs(g.J1[k] - o["J1"][k]) / np.abs(o["J1"][k]))),
+                replay_max_rel=float(err.max()), replay_worst_step=int(err.argmax()), oracle_status=int(st[k]),
+                freerun_first_step_u_gt_1e9=first,
+                freerun_u_maxrel=float(diff_u.max())))
+        rep["replay_max_rel"] = max(x["replay_max_rel"] for x in rep["replay"])
+    return rep
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--threads", type=int, default=16)
+    a = ap.parse_args()
+    rep = compare(a.threads)
+    s = json.dumps(rep, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s)
+
+
+if __name__ == "__main__":
+    main()
