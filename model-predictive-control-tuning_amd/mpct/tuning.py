@@ -195,26 +195,64 @@ def vns2(par: TuningPar, evaluate, fv: float):
     return np.array(N), np.array(Nu), Xv1, Xv2, fv, fv, n_evals
 
 
+class StaleRows:
+    """VNS2.m:148-165: a square plant's VNS runs one closed loop per output i inside try/catch and
+    copies row i of Xy / Xu / Xyma / Xuma from simulation i only when it succeeds (:157-160).  A
+    failed simulation leaves row i as the last successful evaluation set it, so the neighbour's F
+    (:172-195) mixes rows of different neighbours.  Row i enters F only through
+    T_i = j21_i + j22_i + Jnu_i, so the state is the last T per row.  The rows are never
+    initialised: MATLAB zero-fills rows below an assigned one (T_i0 = sum_{t >= inK} Yref_i(t)^2:
+    Xy = Xyma = Xuma = 0), and while fewer than my rows exist :173 (Xy - Yref) throws, which
+    ends the reference's run; here that neighbour scores NaN (never taken).
+    score(N1, terms, ok) -> F = sum_i T_i + N(1) with terms = T of this neighbour's simulations
+    and ok = which of them succeeded; call reset() at the start of every VNS2 pass."""
+
+    def __init__(self, init_terms):
+        self.init = np.asarray(init_terms, dtype=float)
+        self.reset()
+
+    def reset(self):
+        self.last = self.init.copy()
+        self.nrows = 0
+
+    def score(self, N1, terms, ok):
+        terms = np.asarray(terms, dtype=float)
+        ok = np.asarray(ok, dtype=bool)
+        self.last[ok] = terms[ok]
+        if ok.any():
+            self.nrows = max(self.nrows, int(np.nonzero(ok)[0].max()) + 1)
+        if self.nrows < self.last.size:
+            return math.nan
+        return float(self.last.sum()) + N1
+
+
 class _Miss(Exception):
     pass
 
 
-def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512):
+def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512, stale=None):
     """vns2 with every neighbour scored in GPU batches and the SAME decisions as the sequential
     search.  A speculative pass replays the search from the start with the scores known so far;
     unknown neighbours are taken as non-improving and collected, then scored together in one
-    batch (batch_evaluate(list of (N, Nu)) -> list of F).  Replays repeat until a pass needs
-    nothing unknown; every decision of the final pass was taken on real scores, and speculated
-    neighbours never change the search state (a rejected neighbour is reverted), so the result
-    equals the sequential search's.  Returns vns2's tuple plus the number of batches."""
+    batch (batch_evaluate(list of (N, Nu)) -> list of F, or with ``stale`` (StaleRows) a list of
+    (terms, ok) per neighbour, F then following VNS2.m's stale-row semantics in evaluation order).
+    Replays repeat until a pass needs nothing unknown; every decision of the final pass was taken
+    on real scores (and real stale-row state), and speculated neighbours never change the search
+    state (a rejected neighbour is reverted), so the result equals the sequential search's.
+    Returns vns2's tuple plus the number of batches."""
     cache = {}
     n_batches = 0
     while True:
         pending = []
+        if stale is not None:
+            stale.reset()
 
         def spec(N, Nu):
             key = (N, Nu)
             if key in cache:
+                if stale is not None:
+                    terms, ok = cache[key]
+                    return stale.score(N[0], terms, ok)
                 return cache[key]
             if key not in pending and len(pending) < max_batch:
                 pending.append(key)
@@ -226,7 +264,10 @@ def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512
         scores = batch_evaluate(pending)
         n_batches += 1
         for key, F in zip(pending, scores):
-            cache[key] = float(F) if np.isfinite(F) else math.nan
+            if stale is not None:
+                cache[key] = F
+            else:
+                cache[key] = float(F) if np.isfinite(F) else math.nan
 
 
 # --------------------------------------------------------------------------------------------
@@ -239,7 +280,10 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     (MPCTuning.m:88-91: 'DiffMinChange', 0.5); each Jacobian is ONE batch of my+ny+1 closed
     loops.  batch_j1(X rows) -> J1 rows (GAM_fun.m:55-116 for each row).  MATLAB's SQP internals
     are not public: parity with fgoalattain's iterate sequence is unpinned; the goal-attainment
-    formulation and options are the reference's.  Returns (x, attainfactor, last_J1, n_batches)."""
+    formulation and options are the reference's.  Returns (x, attainfactor, J1(x), n_batches,
+    last_eval): last_eval is the J1 of the LAST point the search evaluated, in evaluation order
+    (a Jacobian batch evaluates x, then x + h_k e_k for k = 0..n-1, as MATLAB's forward
+    differences do) -- the value GAM_fun.m:114 leaves in the global F that MPC_TFob.m:104 reads."""
     from scipy.optimize import minimize
 
     my, ny = par.my, par.ny
@@ -248,6 +292,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     cache = {}
     nb = [0]
     last = [None]
+    last_eval = [None]
 
     def evals(X):
         keys = [tuple(np.round(x, 15)) for x in X]
@@ -257,6 +302,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
             nb[0] += 1
             for i, j in zip(todo, J):
                 cache[keys[i]] = np.asarray(j, dtype=float)
+            last_eval[0] = cache[keys[todo[-1]]]   # a cached point is not re-evaluated in MATLAB either
         return [cache[k] for k in keys]
 
     def fd_points(x):
@@ -294,6 +340,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     res = minimize(lambda z: z[-1], z0, jac=lambda z: np.eye(n + 1)[-1], method="SLSQP",
                    constraints=cons, bounds=bounds, options={"maxiter": max_iter, "ftol": ftol})
     x = np.maximum(res.x[:-1], par.lb1)
+    final_eval = last_eval[0]   # the search's own last evaluation, before the report below
     Fx = F(x)
     attain = float(np.max(np.abs(Fx - goal) / w))
     if best[1] is not None and best[0] < attain:
@@ -303,28 +350,32 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
         x = np.maximum(best[1], par.lb1)
         Fx = F(x)
         attain = float(np.max(np.abs(Fx - goal) / w))
-    return x, attain, Fx, nb[0]
+    return x, attain, Fx, nb[0], final_eval
 
 
 # --------------------------------------------------------------------------------------------
-def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400):
+def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400,
+             fgam_from: str = "last_eval", stale=None):
     """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
-    improve.  Quirks kept: Fgam = round(sum(F), 2) of the GAM cost (MPC_TFob.m:104, here at the
-    returned point); OV weights the user set to 0 stay 0 (:83-93); the returned delta/lambda are
-    the LAST GAM result, not the best (:134-135).  Returns (N, Nu, lam, delta, Fvns, Fvf, fv)."""
+    improve.  Quirks kept: Fgam = round(sum(F), 2) where F is the global GAM_fun.m:114 set on its
+    LAST call (MPC_TFob.m:104), i.e. the J1 of fgoalattain's last evaluated point, not of the
+    returned XOt (fgam_from="returned" takes the returned point instead); OV weights the user set
+    to 0 stay 0 (:83-93); the returned delta/lambda are the LAST GAM result, not the best
+    (:134-135); VNS2's stale rows on a failed simulation (``stale``, see StaleRows).
+    Returns (N, Nu, lam, delta, Fvns, Fvf, fv)."""
     my = par.my
     Fva, Fvf = 10e8, 1e15
     hi = 0
     delta = lam = None
     Fvns = fv
     while True:
-        x, attain, Fx, _ = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter)
+        x, attain, Fx, _, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter)
         x = x.copy()
         x[:my][par.ov_zero] = 0.0
         par.x0 = x
         delta = np.abs(x[:my])
         lam = np.abs(x[my:])
-        Fgam = round(float(np.sum(Fx)), 2)
+        Fgam = round(float(np.sum(Flast if fgam_from == "last_eval" and Flast is not None else Fx)), 2)
         if log:
             log("Fgam=%g; Delta=%s; Lambda=%s" % (Fgam, delta, lam))
         if Fgam >= Fvf:
@@ -336,7 +387,7 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
         def bv(keys, _d=par.delta, _l=par.lam):
             return batch_vns(keys, _d, _l)
 
-        N, Nu, Xv1, Xv2, Fvns, fv, _, _ = vns2_batched(par, bv, fv)
+        N, Nu, Xv1, Xv2, Fvns, fv, _, _ = vns2_batched(par, bv, fv, stale=stale)
         if Fvns < Fva:
             Fva = Fvns
             par.N, par.Nu, par.Xv1, par.Xv2 = N, Nu, Xv1, Xv2
@@ -435,27 +486,48 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None, md
         J1[failed(res.status)] = np.nan
         return J1
 
-    def batch_vns(keys, delta, lam):
+    def vns_terms(keys, delta, lam):
         C = len(keys)
         N2 = np.array([max(k[0]) for k in keys], dtype=np.int32)
         Nu = np.array([max(k[1]) for k in keys], dtype=np.int32)
         d = np.tile(np.asarray(delta, dtype=float), (C, 1))
         l = np.tile(np.asarray(lam, dtype=float), (C, 1))
         F, j21, j22, jnu, res = vns_objective(sc, N2, Nu, d, l, device=device, refs=vns_refs, mdv=mdv)
-        bad = failed(res.status).reshape(C, -1).any(axis=1)
-        return np.where(bad, np.nan, F)
+        return F, j21, j22, jnu, failed(res.status).reshape(C, -1)
 
+    def batch_vns(keys, delta, lam):
+        F, j21, j22, jnu, bad = vns_terms(keys, delta, lam)
+        return np.where(bad.any(axis=1), np.nan, F)
+
+    def batch_vns_rows(keys, delta, lam):
+        """Square plants: per neighbour (T, ok) with T_i = j21_i + j22_i + Jnu_i of simulation i
+        and ok_i = simulation i succeeded, for StaleRows (VNS2.m:151-163)."""
+        F, j21, j22, jnu, bad = vns_terms(keys, delta, lam)
+        T = j21 + j22 + jnu
+        return [(T[k], ~bad[k]) for k in range(len(keys))]
+
+    batch_vns.rows = batch_vns_rows if my == ny else None
     return batch_j1, batch_vns
+
+
+def stale_rows_for(yref, inK: int = 10) -> StaleRows:
+    """VNS2's row state before its first simulation: zero rows score T_i0 = sum_{t >= inK}
+    Yref_i(t)^2 (Xy = Xyma = Xuma = 0: j21 = 0, Jnu = 0/0 -> 0, VNS2.m:172-191)."""
+    Y = np.asarray(yref, dtype=float)
+    return StaleRows((Y[:, inK - 1:] ** 2).sum(1))
 
 
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
-               gam_max_iter: int = 400, lineal: bool = True, mdv=None):
+               gam_max_iter: int = 400, lineal: bool = True, mdv=None, fgam_from: str = "last_eval",
+               stale_rows: bool = True):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
     lineal = False: a nonlinear (NMPC) scenario (MPCTuning.m:202-250): VNS simulates the driver's
-    setpoint one output at a time instead of unit steps (VNS2.m:67-71,148-155)."""
+    setpoint one output at a time instead of unit steps (VNS2.m:67-71,148-155).
+    fgam_from / stale_rows: the MPC_TFob.m:104 and VNS2.m:151-163 quirks (mpc_tfob, StaleRows);
+    "returned" / False give the round-2 behaviour (Fgam at the returned point, failed -> NaN)."""
     par = TuningPar(my=my, ny=ny, nbp=nbp, nbc=nbc, dmin=dmin, w=w, q0=q0, w0=w0, nit=sc.nit)
     if sc.n2_max < 2 ** par.nbp - 1 or sc.nu_max < 2 ** par.nbc - 1:
         raise ValueError("scenario horizons (n2_max=%d, nu_max=%d) must cover the bit ranges "
@@ -467,8 +539,12 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
         # square: Xsp.*sel one output at a time (VNS2.m:148-155); non-square: Xsp whole (:168)
         vns_refs = vns_refs_nonlinear(r) if my == ny else np.asarray(r, dtype=float)[None]
     batch_j1, batch_vns = engine_evaluators(sc, r, par, device=device, vns_refs=vns_refs, mdv=mdv)
+    stale = None
+    if stale_rows and batch_vns.rows is not None:   # square plants (VNS2.m:148-165)
+        stale = stale_rows_for(sc.yref)
+        batch_vns = batch_vns.rows
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
-                                                  gam_max_iter=gam_max_iter)
+                                                  gam_max_iter=gam_max_iter, fgam_from=fgam_from, stale=stale)
     if save_path:
         save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
     return N, Nu, delta, lam, np.array([Fvns, Fgam])

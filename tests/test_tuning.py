@@ -109,7 +109,7 @@ def test_gam_goal_attainment_synthetic():
 
     F0 = batch_j1(par.x0)[0]
     att0 = np.max(np.abs(F0 - 1e-3) / par.w)
-    x, att, Fx, nb = gam_fgoalattain(par, batch_j1)
+    x, att, Fx, nb, last = gam_fgoalattain(par, batch_j1)
     assert np.all(x >= par.lb1)
     assert att < 0.5 * att0
     assert att == pytest.approx(np.max(np.abs(Fx - 1e-3) / par.w))
@@ -233,7 +233,7 @@ def test_iteration_caps_keep_finite_costs(monkeypatch):
     bj1, bvns = engine_evaluators(_Sc(2, 2), np.zeros((2, 50)), par)
     J = bj1(np.array([[1.0, 1.0, 0.1, 0.1], [0.5, 2.0, 0.2, 0.1]]))
     assert np.all(np.isfinite(J))
-    x, attain, Fx, nb = gam_fgoalattain(par, bj1, max_iter=5)
+    x, attain, Fx, nb, last = gam_fgoalattain(par, bj1, max_iter=5)
     assert np.all(np.isfinite(x)) and np.isfinite(attain) and np.all(np.isfinite(Fx))
     assert np.all(np.isfinite(bvns([((31, 31), (2, 2)), ((15, 15), (3, 3))], [1, 1], [0.1, 0.1])))
     # a fatal bit on any of a candidate's simulations makes its VNS score NaN (never improves)
@@ -283,3 +283,86 @@ def test_nonsquare_vns_and_mdv(monkeypatch):
     assert stub.calls[-1]["v"].shape == (1, 2, 40) and not stub.calls[-1]["open_loop"]
     bvns([((27,) * 7, (2, 2, 2))], np.zeros(7), [0.1] * 3)
     assert stub.calls[-1]["nref"] == 1 and stub.calls[-1]["v"] is not None
+
+
+def test_fgam_is_the_last_evaluated_j1():
+    """MPC_TFob.m:104 computes Fgam = round(sum(F), 2) from the global F that GAM_fun.m:114 set
+    on its LAST call -- fgoalattain's last evaluated point (a forward-difference point when the
+    search stops after a gradient), not the returned XOt.  gam_fgoalattain reports that J1 in
+    evaluation order (a Jacobian batch is x, then x + h_k e_k), and mpc_tfob's stop test uses it."""
+    from mpct.tuning import mpc_tfob
+
+    a = np.array([1.0, 3.0, 0.5])
+
+    def make():
+        calls = []
+
+        def batch_j1(X):
+            X = np.atleast_2d(X)
+            calls.append(X.copy())
+            J0 = (X[:, 0] - a[0]) ** 2 + 0.1 * X[:, 2] ** 2 + 1e-3
+            J1 = (X[:, 1] - a[1]) ** 2 + 0.1 * X[:, 2] ** 2 + 1e-3
+            return np.stack([J0, J1], axis=1)
+        return batch_j1, calls
+
+    par = TuningPar(my=2, ny=1, w=np.array([0.5, 0.5]))
+    par.x0 = np.array([2.0, 2.0, 2.0])
+    bj, calls = make()
+    x, att, Fx, nb, last = gam_fgoalattain(par, bj, max_iter=20)
+    np.testing.assert_array_equal(last, bj(calls[-1][-1:])[0])    # the last row of the last batch
+    assert not np.array_equal(last, Fx)                              # here: not the returned point
+    # mpc_tfob: Fgam of each GAM round from that last evaluation (logged), VNS stub never improves
+    logs = []
+    for mode in ("last_eval", "returned"):
+        p2 = TuningPar(my=2, ny=1, nbp=3, nbc=2, w=np.array([0.5, 0.5]))
+        p2.x0 = np.array([2.0, 2.0, 2.0])
+        bj, calls = make()
+        out = []
+        mpc_tfob(p2, bj, lambda keys, d, l: [math.inf] * len(keys), log=out.append, gam_max_iter=20,
+                 fgam_from=mode)
+        logs.append(float(out[0].split(";")[0].split("=")[1]))
+    assert logs[0] == round(float(np.sum(last)), 2) and logs[1] == round(float(np.sum(Fx)), 2)
+
+
+def test_vns_stale_rows_semantics():
+    """VNS2.m:148-165 square plants: row i of Xy/Xu/Xyma/Xuma is copied from simulation i only
+    when it succeeds; a failed simulation leaves the row of the last successful evaluation, so F
+    mixes neighbours.  Rows never assigned are MATLAB's zero fill (T_i0 = sum Yref_i^2 from inK);
+    while fewer than my rows exist, VNS2.m:173 throws (here NaN, never taken)."""
+    from mpct.tuning import StaleRows, stale_rows_for
+
+    s = StaleRows([10.0, 20.0, 30.0])
+    assert math.isnan(s.score(5, [1, 2, 3], [True, True, False]))     # row 3 never assigned: throws
+    assert s.score(5, [4, 5, 6], [True, False, True]) == 4 + 2 + 6 + 5  # row 2 stale (from the 1st)
+    assert s.score(7, [7, 8, 9], [False, False, False]) == 4 + 2 + 6 + 7
+    s.reset()
+    assert s.score(5, [1, 2, 3], [False, True, True]) == 10 + 2 + 3 + 5  # row 1: zero fill
+    Y = np.zeros((2, 20))
+    Y[0, 9:] = 1.0
+    Y[1, 5:] = 2.0
+    np.testing.assert_allclose(stale_rows_for(Y).init, [11.0, 4.0 * 11])
+
+
+def test_vns2_batched_stale_rows_equals_sequential():
+    """The speculative batched VNS with stale-row scoring takes the sequential search's decisions:
+    a synthetic square plant where some neighbours' simulations fail."""
+    from mpct.tuning import StaleRows
+
+    par = TuningPar(my=3, ny=3, nbp=7, nbc=4, dmin=np.array([6, 3, 0]))
+
+    def rows(N, Nu):
+        T = np.array([(N[0] - 37) ** 2 / 3.0 + (u - 5) ** 2 + 0.01 * u for u in Nu])
+        ok = np.array([(N[0] * 7 + 3 * i + Nu[i]) % 5 != 0 for i in range(3)])
+        return T, ok
+
+    seq_state = StaleRows([50.0, 60.0, 70.0])
+
+    def seq_eval(N, Nu):
+        T, ok = rows(N, Nu)
+        return seq_state.score(N[0], T, ok)
+
+    seq = vns2(par, seq_eval, 1e30)
+    bat = vns2_batched(par, lambda keys: [rows(*k) for k in keys], 1e30, stale=StaleRows([50.0, 60.0, 70.0]))
+    np.testing.assert_array_equal(seq[0], bat[0])
+    np.testing.assert_array_equal(seq[1], bat[1])
+    assert seq[4] == bat[4] and seq[6] == bat[6] and seq[4] < 1e30

@@ -25,12 +25,12 @@ from oracle.scenarios import shell7x5 as o_shell7x5  # noqa: E402
 FIXTURE = os.path.join(ROOT, "tests", "golden", "config3_cband.npz")
 
 
-def compare(threads=16, nrep=48):
+def compare(threads=16, nrep=48, dump=None, feas_tol=0.0):
     d = np.load(FIXTURE)
     sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
     N2, Nu, D, L = config3_grid(1024)
     t0 = time.time()
-    res = eval_batch(sc, N2, Nu, D, L, r[None], v=v[None])
+    res = eval_batch(sc, N2, Nu, D, L, r[None], v=v[None], feas_tol=feas_tol)
     t_gpu = time.time() - t0
     F = res.J1 @ SHELL7_W
     relF = np.abs(F - d["F_full"]) / np.abs(d["F_full"])
@@ -62,7 +62,8 @@ def compare(threads=16, nrep=48):
     if pick.size:
         osc, orr, ov, oyref, fx = o_shell7x5()
         cb = CBand(osc, 200, oyref)
-        g = eval_batch(sc, N2[pick], Nu[pick], D[pick], L[pick], r[None], v=v[None], want_traj=True)
+        g = eval_batch(sc, N2[pick], Nu[pick], D[pick], L[pick], r[None], v=v[None], want_traj=True,
+                       feas_tol=feas_tol)
         du_o, du_a, st = cb.replay(N2[pick], Nu[pick], D[pick], L[pick], orr, ov, g.u, T=200, threads=threads)
         o = cb.eval(N2[pick], Nu[pick], D[pick], L[pick], orr[None], ov[None], want_traj=True, threads=threads)
         for k, c in enumerate(pick):
@@ -77,6 +78,9 @@ def compare(threads=16, nrep=48):
                 freerun_first_step_u_gt_1e9=first,
                 freerun_u_maxrel=float(diff_u.max())))
         rep["replay_max_rel"] = max(x["replay_max_rel"] for x in rep["replay"])
+        if dump:
+            np.savez_compressed(dump, pick=pick, u_gpu=g.u, y_gpu=g.y, u_c=o["u"], J1_gpu_full=res.J1,
+                                it_gpu_full=res.qp_iters)
     return rep
 
 
@@ -84,8 +88,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--dump", default=None, help="npz with the device trajectories of the replayed candidates")
+    ap.add_argument("--feas-tol", type=float, default=0.0, help="device QP feasibility tolerance (0: default 1e-10)")
     a = ap.parse_args()
-    rep = compare(a.threads)
+    rep = compare(a.threads, dump=a.dump, feas_tol=a.feas_tol)
+    rep["feas_tol"] = a.feas_tol
     s = json.dumps(rep, indent=1)
     print(s)
     if a.out:
