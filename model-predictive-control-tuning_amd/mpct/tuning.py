@@ -272,7 +272,7 @@ def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512
 
 # --------------------------------------------------------------------------------------------
 def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_change: float = 0.5,
-                    max_iter: int = 400, ftol: float = 1e-3):
+                    max_iter: int = 400, ftol: float = 1e-3, speculate: bool = True):
     """GAM step of MPC_TFob.m:61-67: fgoalattain(@GAM_fun, x0, goal=0.001, weight=w, lb=1e-5,
     EqualityGoalCount = numel(w)) -- restated as the goal-attainment problem
         min gamma  s.t.  |J1_i(x) - goal| <= w_i * gamma,  x >= lb1
@@ -283,7 +283,12 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     formulation and options are the reference's.  Returns (x, attainfactor, J1(x), n_batches,
     last_eval): last_eval is the J1 of the LAST point the search evaluated, in evaluation order
     (a Jacobian batch evaluates x, then x + h_k e_k for k = 0..n-1, as MATLAB's forward
-    differences do) -- the value GAM_fun.m:114 leaves in the global F that MPC_TFob.m:104 reads."""
+    differences do) -- the value GAM_fun.m:114 leaves in the global F that MPC_TFob.m:104 reads.
+    speculate: every new point the search asks for (a line-search trial) is scored together with
+    its n forward-difference points in one batch, so an accepted step's Jacobian costs no further
+    engine call (one call per SQP iteration instead of two; the n + 1 closed loops of a batch run
+    side by side, so the call's latency barely grows).  The iterates, the Jacobians and last_eval
+    (taken in the search's own request order) are unchanged."""
     from scipy.optimize import minimize
 
     my, ny = par.my, par.ny
@@ -294,20 +299,28 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     last = [None]
     last_eval = [None]
 
-    def evals(X):
-        keys = [tuple(np.round(x, 15)) for x in X]
-        todo = [i for i, k in enumerate(keys) if k not in cache]
-        if todo:
-            J = batch_j1(np.array([X[i] for i in todo]))
-            nb[0] += 1
-            for i, j in zip(todo, J):
-                cache[keys[i]] = np.asarray(j, dtype=float)
-            last_eval[0] = cache[keys[todo[-1]]]   # a cached point is not re-evaluated in MATLAB either
-        return [cache[k] for k in keys]
-
     def fd_points(x):
         h = np.maximum(diff_min_change, np.sqrt(np.finfo(float).eps) * np.abs(x))
         return [x] + [x + h[k] * np.eye(n)[k] for k in range(n)], h
+
+    asked = set()   # points the search itself has requested (MATLAB evaluates each once)
+
+    def evals(X, spec=()):
+        keys = [tuple(np.round(x, 15)) for x in X]
+        todo = [i for i, k in enumerate(keys) if k not in cache]
+        if todo:
+            extra = [p for p in spec if tuple(np.round(p, 15)) not in cache]
+            J = batch_j1(np.array([X[i] for i in todo] + extra))
+            nb[0] += 1
+            for i, j in zip(todo, J):
+                cache[keys[i]] = np.asarray(j, dtype=float)
+            for p, j in zip(extra, J[len(todo):]):
+                cache[tuple(np.round(p, 15))] = np.asarray(j, dtype=float)
+        new = [k for k in keys if k not in asked]
+        if new:   # the search's own last request (a re-request of a known point is no evaluation)
+            last_eval[0] = cache[new[-1]]
+            asked.update(new)
+        return [cache[k] for k in keys]
 
     def jac_F(x):
         pts, h = fd_points(x)
@@ -319,7 +332,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     best = [np.inf, None]   # best attainment factor over the iterates / line-search points
 
     def F(x):
-        v = evals([x])[0]
+        v = evals([x], spec=fd_points(x)[0][1:] if speculate else ())[0]
         last[0] = v
         a = float(np.max(np.abs(v - goal) / w))
         if a < best[0]:
@@ -355,7 +368,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
 
 # --------------------------------------------------------------------------------------------
 def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400,
-             fgam_from: str = "last_eval", stale=None):
+             fgam_from: str = "last_eval", stale=None, gam_speculate: bool = True):
     """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
     improve.  Quirks kept: Fgam = round(sum(F), 2) where F is the global GAM_fun.m:114 set on its
     LAST call (MPC_TFob.m:104), i.e. the J1 of fgoalattain's last evaluated point, not of the
@@ -369,7 +382,7 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
     delta = lam = None
     Fvns = fv
     while True:
-        x, attain, Fx, _, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter)
+        x, attain, Fx, ncalls, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter, speculate=gam_speculate)
         x = x.copy()
         x[:my][par.ov_zero] = 0.0
         par.x0 = x
@@ -377,7 +390,7 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
         lam = np.abs(x[my:])
         Fgam = round(float(np.sum(Flast if fgam_from == "last_eval" and Flast is not None else Fx)), 2)
         if log:
-            log("Fgam=%g; Delta=%s; Lambda=%s" % (Fgam, delta, lam))
+            log("Fgam=%g; Delta=%s; Lambda=%s; GAM engine calls=%d" % (Fgam, delta, lam, ncalls))
         if Fgam >= Fvf:
             hi += 1
         else:
@@ -520,7 +533,7 @@ def stale_rows_for(yref, inK: int = 10) -> StaleRows:
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
                gam_max_iter: int = 400, lineal: bool = True, mdv=None, fgam_from: str = "last_eval",
-               stale_rows: bool = True):
+               stale_rows: bool = True, gam_speculate: bool = True):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
@@ -544,7 +557,8 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
         stale = stale_rows_for(sc.yref)
         batch_vns = batch_vns.rows
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
-                                                  gam_max_iter=gam_max_iter, fgam_from=fgam_from, stale=stale)
+                                                  gam_max_iter=gam_max_iter, fgam_from=fgam_from, stale=stale,
+                                                  gam_speculate=gam_speculate)
     if save_path:
         save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
     return N, Nu, delta, lam, np.array([Fvns, Fgam])

@@ -308,9 +308,16 @@ def test_fgam_is_the_last_evaluated_j1():
     par = TuningPar(my=2, ny=1, w=np.array([0.5, 0.5]))
     par.x0 = np.array([2.0, 2.0, 2.0])
     bj, calls = make()
-    x, att, Fx, nb, last = gam_fgoalattain(par, bj, max_iter=20)
+    x, att, Fx, nb, last = gam_fgoalattain(par, bj, max_iter=20, speculate=False)
     np.testing.assert_array_equal(last, bj(calls[-1][-1:])[0])    # the last row of the last batch
     assert not np.array_equal(last, Fx)                              # here: not the returned point
+    # speculation (each trial point scored with its forward-difference points) changes neither
+    # the iterates nor the last requested evaluation, and needs fewer engine calls
+    bj2, calls2 = make()
+    x2, att2, Fx2, nb2, last2 = gam_fgoalattain(par, bj2, max_iter=20, speculate=True)
+    np.testing.assert_array_equal(x2, x)
+    np.testing.assert_allclose(last2, last, rtol=1e-12)   # the stub's numpy rounding varies with the batch
+    assert nb2 < nb
     # mpc_tfob: Fgam of each GAM round from that last evaluation (logged), VNS stub never improves
     logs = []
     for mode in ("last_eval", "returned"):
