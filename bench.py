@@ -171,6 +171,39 @@ def other_cpu_baseline(workload, N2, Nu, d, l, refs, J1, st, seconds):
     return {"value": done / tc, "unit": "sims/s", "cores": 1, "kind": "port", "sample": sample}
 
 
+def lib_sha256() -> str:
+    """sha256 of the libmpct.so this process loaded (mpct._lib.lib_path())."""
+    import hashlib
+
+    from mpct import _lib
+
+    with open(_lib.lib_path(), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(C, n2, nu):
+    """roofline.traffic from the committed PMC pass (profiles/pmc_latest.json, written by
+    tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes) -- accepted only
+    when that pass profiled this very library (same sha256) on this workload; otherwise None.
+    Returns (bytes per launch | None, source note)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(pmc):
+        return None, "no PMC pass committed"
+    try:
+        with open(pmc) as f:
+            pj = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable profiles/pmc_latest.json"
+    mine = lib_sha256()
+    src = "profiles/%s_pmc.json" % pj.get("tag", "?")
+    if pj.get("lib_sha256") != mine:
+        return None, "%s profiled libmpct.so sha256 %s, this run loaded %s: not used" % (
+            src, str(pj.get("lib_sha256"))[:16], mine[:16])
+    if (pj.get("candidates"), pj.get("n2"), pj.get("nu")) != (C, n2, nu):
+        return None, "%s is for another workload: not used" % src
+    return pj.get("hbm_bytes_per_launch"), "%s (PMC pass of this libmpct.so, sha256 %s)" % (src, mine[:16])
+
+
 def cpu_model() -> str:
     """The host CPU's model name (report the baseline's cores and CPU model)."""
     try:
@@ -296,16 +329,7 @@ def main():
             tdist.destroy_process_group()
         return
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                pj = json.load(f)
-            if pj.get("candidates") == C and pj.get("n2") == args.n2 and pj.get("nu") == args.nu:
-                traffic = pj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_source = pmc_traffic(C, args.n2, args.nu)
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -362,7 +386,7 @@ def main():
                    "candidates_per_gpu": C, "N2": args.n2, "Nu": args.nu, "nit": sc.nit,
                    "parallelism": "dp%d" % world},
         "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": kernel_name, "kernel_ms": kms,
                      "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as,
                      "bound_note": "FP64 vector ALU issue + per-step dependent latency (no MFMA on this path: "

@@ -10,6 +10,7 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 cd /tmp
 BENCH=(python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline)
+sha256sum "$R/model-predictive-control-tuning_amd/csrc/libmpct.so" > "$O/lib_sha256.txt"
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   (cd "$R" && timeout -k 10 420 python3 -m pytest tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1) \

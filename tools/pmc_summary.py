@@ -1,7 +1,8 @@
 """Turn a gpurun_out/<tag>/ evidence pass (tools/gpu_profile.sh) into the committed summaries:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_pmc.json           per-launch FETCH_SIZE / WRITE_SIZE of the closed-loop kernel
-  profiles/pmc_latest.json          what bench.py reads for roofline.traffic
+  profiles/pmc_latest.json          what bench.py reads for roofline.traffic (keyed by the
+                                    profiled libmpct.so's sha256)
   profiles/<tag>_bench.json         the bench line of the same pass
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM
@@ -55,6 +56,9 @@ def main():
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
         "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes x1024",
+        # the library the counter passes profiled (tools/gpu_profile.sh records it on the box);
+        # bench.py uses hbm_bytes_per_launch only when the library it loads has this hash
+        "lib_sha256": open(os.path.join(src, "lib_sha256.txt")).read().split()[0],
     }
     for name in (a.tag + "_pmc.json", "pmc_latest.json"):
         with open(os.path.join(dst, name), "w") as f:
