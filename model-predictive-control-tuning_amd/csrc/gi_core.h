@@ -4,9 +4,6 @@
 #pragma once
 #include "wave_ops.h"
 
-#ifndef MPCT_BACKSUB_PIPE
-#define MPCT_BACKSUB_PIPE 0  // gi_backsub with its LDS loads one step ahead
-#endif
 #ifndef MPCT_QP_FASTDIV
 #define MPCT_QP_FASTDIV 1  // QP step lengths, Householder / Givens scalars by rcp_nr / rsq_nr (0: IEEE / and sqrt)
 #endif
@@ -54,9 +51,11 @@ struct RowCons {
 // lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
 // and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
 // convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
-// R^-1 (re-adding the set) after MPCT_GI_REBUILD * M rotations (gpc_qp.h, 32M), which bounds the
-// orthogonality drift of the rotated J (unbounded drift measured 3.5e-5 relative on the metric
-// grid; with the rebuild 7.5e-10).
+// R^-1 (re-adding the set) after MPCT_GI_REBUILD * M rotations (gpc_qp.h: 32 M in the M <= 16
+// class, 8 M above), which bounds the orthogonality drift of the rotated J.  Without a rebuild
+// the metric grid drifted to 3.5e-5 relative; the 7.5e-10 bound was measured at the original
+// 4 M interval (C prototype).  At 32 M the metric grid's J1 still equals the C
+// port to 3.2e-9 (the same figure as at 4 M and 8 M); the wider classes keep 8 M.
 template <int MAXM>
 struct GIState {
   double rdg;       // 1 / R_A(lane, lane)
@@ -124,21 +123,6 @@ template <int MAXM>
 __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
   const int lane = qp_lane();
   double ck = lane < S.q ? c : 0.0, rk = 0.0;
-#if MPCT_BACKSUB_PIPE
-  // the next column's R_A entry is loaded one step ahead, so its LDS latency overlaps this
-  // step's broadcast chain (only rows < q read: the others never update)
-  const bool rl = lane < S.q;
-  int w = S.q - 1;
-  double an = (w >= 0 && rl) ? sRA[lane * M + w] : 0.0;
-  for (; w >= 0; --w) {
-    const double a = an;
-    if (w > 0 && rl) an = sRA[lane * M + w - 1];
-    const double rw = bcast(ck * S.rdg, w);
-    if (lane == w) rk = rw;
-    if (lane < w) ck -= a * rw;
-  }
-  return rk;
-#endif
   for (int w = S.q - 1; w >= 0; --w) {
     const double rw = bcast(ck * S.rdg, w);
     if (lane == w) rk = rw;

@@ -41,12 +41,6 @@
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
 #endif
-#ifndef MPCT_PRIO
-#define MPCT_PRIO 0  // wave issue priority for the heaviest slots (1: top 1/16, 2: graded 1/16, 1/4, 1/2)
-#endif
-#ifndef MPCT_UUPD_DEFER
-#define MPCT_UUPD_DEFER 0  // the u update of step t at the top of step t+1 (one LDS hand-off fewer per step)
-#endif
 
 namespace mpct {
 
@@ -131,15 +125,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const int kref = (int)(slot - cs * nref);
   const long long c = perm ? (long long)perm[cs] : cs;
   const long long sim = c * nref + kref;
-#if MPCT_PRIO
-  // issue priority by estimated work: the heaviest slots of an ordered launch (experiment knob)
-  if (perm) {
-    const long long tot = C * nref;
-    if (slot < tot / 16) __builtin_amdgcn_s_setprio(3);
-    else if (MPCT_PRIO > 1 && slot < tot / 4) __builtin_amdgcn_s_setprio(2);
-    else if (MPCT_PRIO > 1 && slot < tot / 2) __builtin_amdgcn_s_setprio(1);
-  }
-#endif
   const int my = sc.my, nu = sc.nu, nin = sc.nin, nit = sc.nit, nx = sc.nx, ne = sc.ne;
   const int N2 = N2v[c], Nu = Nuv[c];
   const int M = nu * Nu;
@@ -505,9 +490,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     // SGPR budget spills to VGPR lanes and reloads (v_readlane) several times per step
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    // MPCT_UUPD_DEFER: step t-1's u update runs here, under the same LDS hand-off as the inputs
-    // of step t (sxc still holds step t-1's moves: nothing writes it before the next solve)
-    if (MPCT_UUPD_DEFER && t > 0) u_update(t - 1, ln);
     double r_n = 0.0, yr_n = 0.0;
     if (lane < my && t + 1 < nit) {  // prefetch t+1
       r_n = rr[lane * nit + t + 1];
@@ -638,17 +620,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     lds_sync();
     PSTAMP(PROF_YUPD);
     if (!(MPCT_EXP_SKIP & 4)) solve_step();
-    if (!MPCT_UUPD_DEFER) {
-      u_update(t, ln);
-      lds_sync();
-    }
+    u_update(t, ln);
+    lds_sync();
     r_t = r_n;
     yr_t = yr_n;
     PSTAMP(PROF_UUPD);
-  }
-  if (MPCT_UUPD_DEFER && nit > 0) {
-    int ln = lane;
-    u_update(nit - 1, ln);
   }
 #ifdef MPCT_PROFILE
   if (lane == 0 && out.prof)

@@ -13,8 +13,14 @@
 #endif
 
 #ifndef MPCT_GI_REBUILD
-#define MPCT_GI_REBUILD 32  // J (and R_A) rebuilt from R^-1 after this many x M rotations (DESIGN.md §5;
-                            // 8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than 8 M; same parity, tools/ab_variants.sh)
+#define MPCT_GI_REBUILD 32  // J (and R_A) rebuilt from R^-1 after this many x M rotations in the M <= 16
+                            // class (8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than
+                            // 8 M, same metric-grid parity, profiles/r02k_gib_rebuild_ab.txt)
+#endif
+#ifndef MPCT_GI_REBUILD_WIDE
+#define MPCT_GI_REBUILD_WIDE 8  // the <32> / <64> classes (config 4's M > 16 draws, long horizons):
+                                // longer active sets apply more rotations per add, and 32 M was only
+                                // measured on the metric class, so they keep the 8 M interval
 #endif
 
 namespace mpct {
@@ -54,8 +60,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
   double* sB = MPCT_GI_B ? Q.b : nullptr;
   double* sw = Q.w;
   if (!row) up_row = 0.0;
-  int rl = rc.l;  // the lane's position in its MV block
-  if (MPCT_QP_OPAQUE) asm volatile("" : "+v"(rl));
+  const int rl = rc.l;  // the lane's position in its MV block
   const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
   auto slacks = [&](double x, double s[4]) {
     const double pre = block_prefix<MAXM>(x, rl, Nu, row, sxc);
@@ -87,7 +92,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
 #pragma unroll
         for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
       }
-      if (!S.jinit || S.nrot >= MPCT_GI_REBUILD * M) {
+      if (!S.jinit || S.nrot >= (MAXM <= 16 ? MPCT_GI_REBUILD : MPCT_GI_REBUILD_WIDE) * M) {
         // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
         gi_load_rinv<MAXM>(S, sJT, sRi, M, row);

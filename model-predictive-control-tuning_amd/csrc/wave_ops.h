@@ -37,15 +37,9 @@ __device__ __forceinline__ double rsq_nr(double x) {
   return r * fma(-h * r, r, 1.5);
 }
 
-#ifndef MPCT_QP_OPAQUE
-#define MPCT_QP_OPAQUE 0  // QP lane predicates from an opaque lane id (not hoisted out of the step loop)
-#endif
-// lane id for the QP helpers: with MPCT_QP_OPAQUE an opaque copy, so the compiler re-derives the
-// loop-invariant lane predicates where they are used instead of keeping them as SGPR-pair masks
+// lane id for the QP helpers
 __device__ __forceinline__ int qp_lane() {
-  int l = threadIdx.x;
-  if (MPCT_QP_OPAQUE) asm volatile("" : "+v"(l));
-  return l;
+  return threadIdx.x;
 }
 
 __device__ __forceinline__ double bcast(double v, int src) {

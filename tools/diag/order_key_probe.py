@@ -1,7 +1,6 @@
 """Dispatch-order probe of the metric batch with an identity-order build (MPCT_LIB =
 libmpct_ident.so, -DMPCT_ORDER_IDENTITY): kernel time in grid order, in descending order of
-measured QP work, and in descending order of an offline estimate (the permutations in
-tools/diag/metric_perm_*.npy)."""
+measured QP work (qp_iters of a first run, computed here)."""
 import os
 import sys
 
@@ -38,8 +37,9 @@ def timed(perm, reps=7):
     return float(np.median(ts))
 
 
-D = os.path.join(ROOT, "tools", "diag")
+from mpct.engine import eval_batch  # noqa: E402
+
+work = eval_batch(sc, N2, Nu, d, l, r[None]).qp_iters
 print(os.path.basename(os.environ.get("MPCT_LIB", "libmpct.so")))
 print("grid order      %.3f ms" % timed(np.arange(4096)))
-for n in sys.argv[1:] or ("work", "est"):
-    print("%-15s %.3f ms" % ("desc " + n, timed(np.load(os.path.join(D, "metric_perm_%s.npy" % n)))))
+print("desc work       %.3f ms" % timed(np.argsort(-work, kind="stable")))

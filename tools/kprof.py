@@ -11,9 +11,10 @@ from mpct.scenarios import candidate_grid, shell3x3
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 sc, r, yref = shell3x3()
 N2, Nu, d, l = candidate_grid(4096)
-# "heavy": the C candidates the dispatch key ranks heaviest (tools/diag/metric_perm_est.npy)
-sel = (np.load(os.path.join(ROOT, "tools", "diag", "metric_perm_est.npy"))[:C] if "heavy" in sys.argv[2:]
-       else np.arange(C))
+# "heavy": the C candidates with the most measured QP work (a first, unprofiled pass)
+sel = np.arange(C)
+if "heavy" in sys.argv[2:]:
+    sel = np.argsort(-eval_batch(sc, N2, Nu, d, l, r[None]).qp_iters, kind="stable")[:C]
 N2, Nu, d, l = N2[sel], Nu[sel], d[sel], l[sel]
 eval_batch(sc, N2[:64], Nu[:64], d[:64], l[:64], r[None])
 t = time.perf_counter()
