@@ -25,6 +25,9 @@
 #include "gi_core.h"
 #include "gpc_qp.h"
 
+#ifndef MPCT_STAGE_RESULTS
+#define MPCT_STAGE_RESULTS 1  // ordered launches write their cost records XCD-major, then gather (DevResult::stage)
+#endif
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
                              // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
@@ -134,18 +137,35 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 
-  auto write_nan = [&](int status) __attribute__((always_inline)) {
-    if (lane < my) {
-      if (out.J1) out.J1[sim * my + lane] = NAN;
-      if (out.j21) out.j21[sim * my + lane] = NAN;
-      if (out.j22) out.j22[sim * my + lane] = NAN;
+  // the cost record: caller's arrays at `sim`, or staging row xcd_row(slot) (ordered launches)
+  auto put_record = [&](double j1v, double j21v, double j22v, double jnuv, int status, long long itv)
+                        __attribute__((always_inline)) {
+    if (out.stage) {
+      double* row = out.stage + xcd_row(slot, C * nref) * stage_width(my, nu);
+      if (lane < my) {
+        row[lane] = j1v;
+        row[my + lane] = j21v;
+        row[2 * my + lane] = j22v;
+      }
+      if (lane < nu) row[3 * my + lane] = jnuv;
+      if (lane == 0) {
+        row[3 * my + nu] = (double)status;
+        row[3 * my + nu + 1] = (double)itv;
+      }
+      return;
     }
-    if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = NAN;
+    if (lane < my) {
+      if (out.J1) out.J1[sim * my + lane] = j1v;
+      if (out.j21) out.j21[sim * my + lane] = j21v;
+      if (out.j22) out.j22[sim * my + lane] = j22v;
+    }
+    if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = jnuv;
     if (lane == 0) {
       if (out.status) out.status[sim] = status;
-      if (out.qp_iters) out.qp_iters[sim] = 0;
+      if (out.qp_iters) out.qp_iters[sim] = itv;
     }
   };
+  auto write_nan = [&](int status) __attribute__((always_inline)) { put_record(NAN, NAN, NAN, NAN, status, 0); };
   if (N2 <= 0) {
     if (first) write_nan(MPCT_ST_SKIPPED_);
     return;
@@ -632,19 +652,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #endif
 
   // ------------------------------------------------------------------ results
-  if (lane < my) {
-    if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;
-    if (out.J1) out.J1[sim * my + lane] = j1;
-    if (out.j22) out.j22[sim * my + lane] = j22;
-    if (out.j21) out.j21[sim * my + lane] = (EXT && o.open_loop) ? j21 : NAN;
-  }
-  if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = (EXT && o.open_loop) ? jnu : NAN;
+  if (lane < my && !isfinite(j1)) st |= MPCT_ST_NONFINITE_;
   const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
-  if (lane == 0) {
-    const int s = st | (nf ? MPCT_ST_NONFINITE_ : 0);
-    if (out.status) out.status[sim] = s;
-    if (out.qp_iters) out.qp_iters[sim] = iters;
-  }
+  put_record(j1, (EXT && o.open_loop) ? j21 : NAN, j22, (EXT && o.open_loop) ? jnu : NAN,
+             st | (nf ? MPCT_ST_NONFINITE_ : 0), iters);
 }
 
 }  // namespace mpct
@@ -656,6 +667,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #include "work_order.h"
 #include "launch_fan.h"
 
+#ifndef MPCT_STAGE_RESULTS
+#define MPCT_STAGE_RESULTS 1  // ordered launches write their cost records XCD-major, then gather (DevResult::stage)
+#endif
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
                              // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
@@ -733,6 +747,13 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
         order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err, &sc, nref, r);
     if (rc) return rc;
   }
+  // ordered launches stage their cost records XCD-major and gather them into the caller's order
+  // afterwards (DevResult::stage): full-line writes instead of 24-B pieces from every L2
+  DevResult lo = out;
+  if (perm && MPCT_STAGE_RESULTS) {
+    const int rs = order_stage(*wo, C * nref, sc.my, sc.nu, &lo.stage, err);
+    if (rs) return rs;
+  }
   int rc = 0;
   FanScope fs(top_class(maxM) > 16 ? fan : nullptr, stream);
   int k = 0, mlo = 0;
@@ -743,13 +764,14 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     }
     const hipStream_t st = fs.stream(k);
     const int first = k == 0;
-    if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
-    else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
-    else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, perm, mlo, first, st, err);
+    if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
+    else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
+    else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     mlo = cls;
     ++k;
   }
   fs.join();
+  if (rc == 0 && lo.stage) rc = unpermute_results(*wo, C, nref, sc.my, sc.nu, out, stream, err);
   if (perm) order_mark_used(*wo, stream);
   return rc;
 }

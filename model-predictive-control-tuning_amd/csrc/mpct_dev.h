@@ -11,6 +11,9 @@ namespace mpct {
 struct WorkOrder {
   void* buf = nullptr;
   size_t bytes = 0;
+  int* inv = nullptr;       // candidate -> slot (inverse of the last permutation), inside buf
+  void* stage = nullptr;    // staging rows of the ordered launch's cost records (DevResult::stage)
+  size_t stage_bytes = 0;
   hipEvent_t used = nullptr;
   bool pending = false;  // `used` has been recorded
 };
@@ -108,7 +111,22 @@ struct DevResult {
   int64_t* qp_iters;
   double *y, *u, *ys, *uopt;
   unsigned long long* prof;  // diagnostic builds only (-DMPCT_PROFILE): [sim][8] cycle sums
+  // ordered launches: the cost record of workgroup slot k goes to staging row xcd_row(k) instead
+  // of the caller's arrays, and unpermute_results gathers it back into the caller's order.  The
+  // workgroups of a launch are dealt to the 8 XCDs round robin, so XCD x's slots fill one
+  // contiguous block of rows and every 128-B line is written from one L2; written straight to the
+  // caller's (permuted) index, a line collects 24-B pieces from up to 8 L2s and each writes back
+  // its partial copy (5x the result bytes in WRITE_SIZE, profiles/r02m_pmc.json).
+  double* stage = nullptr;
 };
+
+constexpr int kXcds = 8;
+// staging row of workgroup slot k of an S-slot launch: XCD-major
+__host__ __device__ inline long long xcd_row(long long k, long long S) {
+  return (k % kXcds) * ((S + kXcds - 1) / kXcds) + k / kXcds;
+}
+// staging row layout: J1 [my] | j21 [my] | j22 [my] | Jnu [nu] | status | qp_iters, padded even
+__host__ __device__ inline int stage_width(int my, int nu) { return (3 * my + nu + 2 + 1) & ~1; }
 
 // section ids of the diagnostic in-kernel stamps
 enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,

@@ -34,6 +34,13 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
 int rank_device(const double* costs, long long C, int k, const double* w, int* perm, hipStream_t stream,
                 std::string* err);
 
+// staging rows for the cost records of an ordered launch of S simulations (DevResult::stage), and
+// the gather of those rows back into the caller's order (one thread per simulation, contiguous
+// writes); enqueue the gather after every launch of the batch
+int order_stage(WorkOrder& wo, long long S, int my, int nu, double** stage, std::string* err);
+int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const DevResult& out,
+                      hipStream_t stream, std::string* err);
+
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);
 void order_release(WorkOrder& wo);

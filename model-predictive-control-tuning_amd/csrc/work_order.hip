@@ -268,6 +268,11 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   }
 }
 
+__global__ void invert_perm(const int* __restrict__ perm, long long C, int* __restrict__ inv) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < C) inv[perm[i]] = (int)i;
+}
+
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
                      const DevScenario* sc, int nref, const double* r) {
@@ -332,7 +337,63 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
     *err = "hipcub::DeviceRadixSort::SortPairs failed";
     return -3;
   }
+  // the inverse permutation (candidate -> slot) into the free key buffer, for unpermute_results
+  int* inv = reinterpret_cast<int*>(kin);
+  hipLaunchKernelGGL(invert_perm, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, iout, C, inv);
+  if (hipGetLastError() != hipSuccess) {
+    *err = "invert_perm launch failed";
+    return -3;
+  }
+  wo.inv = inv;
   *perm = iout;
+  return 0;
+}
+
+int order_stage(WorkOrder& wo, long long S, int my, int nu, double** stage, std::string* err) {
+  const size_t need = (size_t)kXcds * ((S + kXcds - 1) / kXcds) * stage_width(my, nu) * sizeof(double);
+  if (need > wo.stage_bytes) {
+    if (wo.stage) (void)hipFree(wo.stage);
+    wo.stage = nullptr;
+    wo.stage_bytes = 0;
+    if (hipMalloc(&wo.stage, need) != hipSuccess) {
+      *err = "hipMalloc failed (result staging)";
+      return -2;
+    }
+    wo.stage_bytes = need;
+  }
+  *stage = static_cast<double*>(wo.stage);
+  return 0;
+}
+
+// thread s = c*nref + k of the caller's order reads the staging row of slot inv[c]*nref + k
+__global__ void unpermute_kernel(const double* __restrict__ stage, const int* __restrict__ inv, long long C,
+                                 int nref, int my, int nu, DevResult out) {
+  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long S = C * nref;
+  if (s >= S) return;
+  const long long c = s / nref;
+  const long long slot = (long long)inv[c] * nref + (s - c * nref);
+  const double* row = stage + xcd_row(slot, S) * stage_width(my, nu);
+  for (int i = 0; i < my; ++i) {
+    if (out.J1) out.J1[s * my + i] = row[i];
+    if (out.j21) out.j21[s * my + i] = row[my + i];
+    if (out.j22) out.j22[s * my + i] = row[2 * my + i];
+  }
+  if (out.Jnu)
+    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = row[3 * my + i];
+  if (out.status) out.status[s] = (int)row[3 * my + nu];
+  if (out.qp_iters) out.qp_iters[s] = (long long)row[3 * my + nu + 1];
+}
+
+int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const DevResult& out,
+                      hipStream_t stream, std::string* err) {
+  const long long S = C * nref;
+  hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream,
+                     static_cast<const double*>(wo.stage), wo.inv, C, nref, my, nu, out);
+  if (hipGetLastError() != hipSuccess) {
+    *err = "unpermute_results launch failed";
+    return -3;
+  }
   return 0;
 }
 
@@ -389,6 +450,7 @@ int rank_device(const double* costs, long long C, int k, const double* w, int* p
 
 void order_release(WorkOrder& wo) {
   if (wo.buf) (void)hipFree(wo.buf);
+  if (wo.stage) (void)hipFree(wo.stage);
   if (wo.used) (void)hipEventDestroy(wo.used);
   wo = WorkOrder{};
 }
