@@ -41,10 +41,6 @@
 #ifndef MPCT_REG_Y
 #define MPCT_REG_Y 0   // y backward-difference histories in VGPRs (else in LDS; 0 measured faster)
 #endif
-#ifndef MPCT_LANE_HANDOFF
-#define MPCT_LANE_HANDOFF 1  // M <= 16 class, no DTC: step hand-offs by DPP in registers (plant quads,
-                             // MV block leaders) instead of LDS round trips, where the scenario fits
-#endif
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
 #endif
@@ -340,14 +336,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #endif
 
   // per-lane constants of the step loop, defined after the prologue so that they are not live
-  // (and spilled) across its register-heavy QR.
-  // Lane hand-off layout (fast, M <= 16 class without DTC, register-resident plant, nin <= 4,
-  // my <= 8): plant entry (i, j) of copy c on lane 32c + 4i + j, so output i is a quad_perm sum
-  // and its state update runs on the quad's first lane 4i; MV n lives on the first lane n*Nu of
-  // its QP block, which holds the move the QP leaves there, and every lane of the block keeps
-  // u(t-1) in a register (segmented DPP broadcast of the move).  No LDS round trip between the
-  // plant, the output update and the MV update.  Otherwise: entry e on lane e, output i on lane
-  // i, MV n on lane n, hand-offs through LDS.
+  // (and spilled) across its register-heavy QR
+  const int yoff_i = lane < my ? sc.yoff[lane] : 0;
+  const int nyh_i = lane < my ? sc.nyhi[lane] : 0;
+  const int upoff_n = lane < nu ? sc.upoff[lane] : 0;
+  const int dum_n = lane < nu ? sc.dum[lane] : 0;
   RowCons rcn;
   rcn.n = lane < M ? lane / Nu : 0;
   rcn.l = lane < M ? lane - rcn.n * Nu : 0;
@@ -355,23 +348,12 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   rcn.dmax = sc.bnd[nu + rcn.n];
   rcn.umin = sc.bnd[2 * nu + rcn.n];
   rcn.umax = sc.bnd[3 * nu + rcn.n];
-  bool fast = false;
-  if constexpr (MAXM <= 16 && !DTC) fast = MPCT_LANE_HANDOFF && sc.regpath && nin <= 4 && my <= 8;
-  const bool ylane = fast ? ((lane & 3) == 0 && lane < 4 * my) : lane < my;  // output-update lanes
-  const int yi = fast ? (lane >> 2) : lane;                                   // their output
-  const bool ulane = fast ? (lane < M && rcn.l == 0) : lane < nu;             // MV-update lanes
-  const int un_i = fast ? rcn.n : lane;                                       // their MV
-  const int yoff_i = ylane ? sc.yoff[yi] : 0;
-  const int nyh_i = ylane ? sc.nyhi[yi] : 0;
-  const int upoff_n = ulane ? sc.upoff[un_i] : 0;
-  const int dum_n = ulane ? sc.dum[un_i] : 0;
-  const int ecopy = fast ? (lane >> 5) : lane / ne;
-  const int ej = fast ? (lane & 3) : (lane - ecopy * ne) % nin;
-  const int ee = fast ? ((lane & 31) >> 2) * nin + ej : lane - ecopy * ne;
-  const bool ent = fast ? (ej < nin && ((lane & 31) >> 2) < my) : lane < ne * 2;
-  const int e_nb = ent ? sc.pl_nb[pve + ee] : 0;
-  const int e_na = ent ? sc.pl_na[pve + ee] : 0;
-  const int e_off = ent ? sc.pl_off[pve + ee] : 0;
+  const int ecopy = lane / ne;
+  const int ee = lane - ecopy * ne;
+  const int ej = ee % nin;
+  const int e_nb = (lane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
+  const int e_na = (lane < ne * 2) ? sc.pl_na[pve + ee] : 0;
+  const int e_off = (lane < ne * 2) ? sc.pl_off[pve + ee] : 0;
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 8 * M + 16;
   long long iters = 0;
@@ -380,10 +362,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 
   GIState<MAXM> gis;  // active-set factorisation carried across the steps (warm start)
   gi_reset<MAXM>(gis);
-  double upr = 0.0;  // fast layout: u(t-1) of the lane's MV block (lanes < M)
-  // unconstrained minimiser dU = A x, then the QP; the moves return in lanes < M (and in sxc
-  // unless fast)
-  auto solve_step = [&]() __attribute__((always_inline)) -> double {
+  // unconstrained minimiser dU = A x, then the QP; result in sxc
+  auto solve_step = [&]() __attribute__((always_inline)) {
     double xu = 0.0;
     if constexpr (MAXM <= 16) {
       // the four 16-lane rows split A's column pairs; row m of A on lanes m, m+16, m+32, m+48
@@ -401,7 +381,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         }
       }
       xu = row4_sum(a0 + a1);
-      if (!fast && lane < M) sxc[lane] = xu;
+      if (lane < M) sxc[lane] = xu;
       if (lane >= M) xu = 0.0;
     } else if (lane < M) {
       // 16-byte LDS reads: two A entries of this row and two x entries per load
@@ -425,33 +405,26 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       xu = (a0 + a1) + (a2 + a3);
       sxc[lane] = xu;
     }
-    if (!fast) lds_sync();
+    lds_sync();
     PSTAMP(PROF_UNC);
-    double xm = xu;
 #ifndef MPCT_EXP_NOQP
     const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
-    iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? (fast ? upr : suprev[rcn.n]) : 0.0, xu, tol, maxit, &st, gis,
-                         xm, !fast
+    iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
 #ifdef MPCT_PROFILE
                          , pacc, pprev
 #endif
     );
 #endif
     PSTAMP(PROF_QP);
-    return xm;
   };
 
   // ------------------------------------------------------------------ open-loop prediction
   double jnu = 0.0;
   if ((EXT && o.open_loop)) {
     // closedloop_toolbox.m:86-91: initial state (y = 0), reference r(:, end)
-    if (lane < my) sx[sc.yoff[lane]] = -rr[lane * nit + (nit - 1)];
+    if (lane < my) sx[yoff_i] = -rr[lane * nit + (nit - 1)];
     lds_sync();
-    const double x0 = solve_step();
-    if (fast) {
-      if (lane < M) sxc[lane] = x0;
-      lds_sync();
-    }
+    solve_step();
     if (lane < M) {
       double s = 0.0;
       for (int j = lane - rcn.l; j <= lane; ++j) s += sxc[j];
@@ -468,7 +441,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         if (isfinite(xr)) jnu += xr * xr;
       }
     }
-    if (lane < my) sx[sc.yoff[lane]] = 0.0;
+    if (lane < my) sx[yoff_i] = 0.0;
     lds_sync();
     PSTAMP(PROF_OPENLOOP);
   }
@@ -476,7 +449,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   // ------------------------------------------------------------------ closed loop
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
   const int ncopy = (EXT && o.open_loop) ? 2 : 1;
-  const bool is_entry = fast ? (ent && ecopy < ncopy) : lane < ncopy * ne;
+  const bool is_entry = lane < ncopy * ne;
   const double* eb = splb + ee * sc.pl_maxb;
   const double* ea = spla + ee * sc.pl_maxa;
   double* eyh = syeh + lane * kYeHist;
@@ -498,26 +471,16 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const bool regpath = sc.regpath != 0;
   // prefetched per-output signals
   double r_t = 0.0, yr_t = 0.0;
-  if (ylane) {
-    r_t = rr[yi * nit];
-    yr_t = sc.yref[yi * nit];
+  if (lane < my) {
+    r_t = rr[lane * nit];
+    yr_t = sc.yref[lane * nit];
   }
-  // u(t) = u(t-1) + du(t, first move) of MV n: past-control state, plant input ring.  xm: the
-  // moves (lanes < M); fast layout: every lane of block n adds its leader's move to its u(t-1)
-  auto u_update = [&](int t, int ln, double xm) __attribute__((always_inline)) {
-    double du = 0.0, un = 0.0;
-    if (fast) {
-      const bool row = lane < M;
-      du = block_prefix<MAXM>(row && rcn.l == 0 ? xm : 0.0, rcn.l, Nu, row, sxc);
-      if (row) upr += du;
-      un = upr;
-    }
-    if (!(MPCT_EXP_SKIP & 8) && (fast ? ulane : ln < nu)) {
-      const int n = un_i;
-      if (!fast) {
-        du = sxc[n * Nu];
-        un = suprev[n] + du;
-      }
+  // u(t) = u(t-1) + du(t, first move) of MV n = lane: past-control state, plant input ring
+  auto u_update = [&](int t, int ln) __attribute__((always_inline)) {
+    if (!(MPCT_EXP_SKIP & 8) && ln < nu) {
+      const int n = lane;
+      const double du = sxc[n * Nu];
+      const double un = suprev[n] + du;
       if (regpath && MPCT_REG_DU) {  // past-control register in registers, written out whole
 #pragma unroll
         for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
@@ -538,7 +501,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
           out.uopt[(sim * nu + n) * nit + t] = sucum[n * Nu + l];
         }
       }
-      if (!fast) suprev[n] = un;
+      suprev[n] = un;
     }
   };
   for (int t = 0; t < nit; ++t) {
@@ -548,9 +511,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     int ln = lane;
     asm volatile("" : "+v"(ln));
     double r_n = 0.0, yr_n = 0.0;
-    if (ylane && t + 1 < nit) {  // prefetch t+1
-      r_n = rr[yi * nit + t + 1];
-      yr_n = sc.yref[yi * nit + t + 1];
+    if (lane < my && t + 1 < nit) {  // prefetch t+1
+      r_n = rr[lane * nit + t + 1];
+      yr_n = sc.yref[lane * nit + t + 1];
     }
     // inputs at time t that are already known: MDs v(t); open-loop uopt(t)
     if (sc.nd > 0) {
@@ -565,8 +528,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    double yq = 0.0;  // fast layout: the quad's output sum, y_i (copy 0) or ys_i (copy 1)
-    if (!(MPCT_EXP_SKIP & 1) && (fast ? is_entry : ln < ncopy * ne)) {
+    if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double acc;
@@ -587,15 +549,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         acc = a0 + a1;
         eyh[t & (kYeHist - 1)] = acc;
       }
-      if (fast) yq = acc;
-      else sye[lane] = acc;
+      sye[lane] = acc;
     }
-    if (fast) {
-      yq += dppd<kQx1>(yq);  // ((y_i0 + y_i1) + (y_i2 + y_i3)): the entries of output i are one quad
-      yq += dppd<kQx2>(yq);
-    } else {
-      lds_sync();
-    }
+    lds_sync();
     PSTAMP(PROF_PLANT);
     if constexpr (DTC) {
       // predictor model entries on the controller's own input history (OptimalPredictor2.m:
@@ -617,16 +573,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       }
       lds_sync();
     }
-    double ysq = 0.0;
-    if ((EXT && o.open_loop) && fast) ysq = __shfl_xor(yq, 32, 64);  // ys_i from lane 32 + 4i
-    if (!(MPCT_EXP_SKIP & 2) && (fast ? ylane : ln < my)) {
-      const int i = yi;
+    if (!(MPCT_EXP_SKIP & 2) && ln < my) {
+      const int i = lane;
       double y = 0.0;
-      if (fast) {
-        y = yq;
-      } else {
-        for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
-      }
+      for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
       // the measurement driving the free response: y, or the DTC predictor output
       // yp = Gz*u + Fr*(y - Pz*u)  (OptimalPredictor2.m:24-40, DTC_GPC_WW.m:133-142)
       double ym = y;
@@ -679,11 +629,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       if (t >= sc.ink0) j22 += e1 * e1;
       double ysv = 0.0;
       if ((EXT && o.open_loop)) {
-        if (fast) {
-          ysv = ysq;
-        } else {
-          for (int j = 0; j < nin; ++j) ysv += sye[ne + i * nin + j];
-        }
+        for (int j = 0; j < nin; ++j) ysv += sye[ne + i * nin + j];
         if (t >= sc.ink0) j21 += (y - ysv) * (y - ysv);
       }
       if ((EXT && o.want_traj)) {
@@ -693,10 +639,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     }
     lds_sync();
     PSTAMP(PROF_YUPD);
-    double xm = 0.0;
-    if (!(MPCT_EXP_SKIP & 4)) xm = solve_step();
-    u_update(t, ln, xm);
-    if (!fast) lds_sync();  // fast: the next step's first hand-off orders these stores
+    if (!(MPCT_EXP_SKIP & 4)) solve_step();
+    u_update(t, ln);
+    lds_sync();
     r_t = r_n;
     yr_t = yr_n;
     PSTAMP(PROF_UUPD);
@@ -707,11 +652,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #endif
 
   // ------------------------------------------------------------------ results
-  if (fast) {  // the costs of output i sit on lane 4i
-    j1 = __shfl(j1, 4 * lane, 64);
-    j21 = __shfl(j21, 4 * lane, 64);
-    j22 = __shfl(j22, 4 * lane, 64);
-  }
   if (lane < my && !isfinite(j1)) st |= MPCT_ST_NONFINITE_;
   const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
   put_record(j1, (EXT && o.open_loop) ? j21 : NAN, j22, (EXT && o.open_loop) ? jnu : NAN,

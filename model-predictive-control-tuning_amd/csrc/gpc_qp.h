@@ -41,12 +41,10 @@ struct QPBufs {
   double *b, *w;       // B = R_A^-1 and the warm start's w (MPCT_GI_B)
 };
 
-// the QP of one step: unconstrained minimiser xu (lanes < M), u(t-1) of the lane's MV up_row.
-// The optimal moves return in xres (lanes < M) and, with store_x, in Q.xc (which then already
-// holds x_u on entry: the feasible-x_u exit leaves it as it is).
+// the QP of one step: unconstrained minimiser xu (lanes < M), u(t-1) of the lane's MV up_row
 template <int MAXM>
 __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCons& rc, double up_row,
-                     double xu, double tol, int maxit, int* st, GIState<MAXM>& S, double& xres, bool store_x
+                     double xu, double tol, int maxit, int* st, GIState<MAXM>& S
 #ifdef MPCT_PROFILE
                      , unsigned long long* pacc, unsigned long long& pprev
 #endif
@@ -86,10 +84,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
     double s[4];
     slacks(xu, s);
     const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
-    if (__ballot(smin < -tol) == 0) {  // x_u is optimal (with store_x, sxc holds it: solve_step)
-      xres = xu;
-      return 0;
-    }
+    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
     if (S.q == 0) {
       S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
     } else {
@@ -251,11 +246,8 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
     }
     if (it >= maxit || infeas) break;
   }
-  xres = row ? xm : 0.0;
-  if (store_x) {
-    if (row) sxc[lane] = xm;
-    lds_sync();
-  }
+  if (row) sxc[lane] = xm;
+  lds_sync();
   return it;
 }
 
