@@ -316,7 +316,7 @@ def test_fgam_is_the_last_evaluated_j1():
     bj2, calls2 = make()
     x2, att2, Fx2, nb2, last2 = gam_fgoalattain(par, bj2, max_iter=20, speculate=True)
     np.testing.assert_array_equal(x2, x)
-    np.testing.assert_allclose(last2, last, rtol=1e-12)   # the stub's numpy rounding varies with the batch
+    np.testing.assert_allclose(last2, last, rtol=1e-9)   # points matched to 13 digits (stub rounding too)
     assert nb2 < nb
     # mpc_tfob: Fgam of each GAM round from that last evaluation (logged), VNS stub never improves
     logs = []
