@@ -272,8 +272,7 @@ def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512
 
 # --------------------------------------------------------------------------------------------
 def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_change: float = 0.5,
-                    max_iter: int = 400, ftol: float = 1e-3, speculate: bool = True, ladder: int = 3,
-                    trace=None):
+                    max_iter: int = 400, ftol: float = 1e-3, speculate: bool = False):
     """GAM step of MPC_TFob.m:61-67: fgoalattain(@GAM_fun, x0, goal=0.001, weight=w, lb=1e-5,
     EqualityGoalCount = numel(w)) -- restated as the goal-attainment problem
         min gamma  s.t.  |J1_i(x) - goal| <= w_i * gamma,  x >= lb1
@@ -285,16 +284,14 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     last_eval): last_eval is the J1 of the LAST point the search evaluated, in evaluation order
     (a Jacobian batch evaluates x, then x + h_k e_k for k = 0..n-1, as MATLAB's forward
     differences do) -- the value GAM_fun.m:114 leaves in the global F that MPC_TFob.m:104 reads.
-    speculate: every new point the search asks for (a line-search trial x_k + s) is scored in one
-    batch together with its n forward-difference points and, with ``ladder`` = K, the next K
-    trials SLSQP's inexact line search takes when it backs off to its floor step (x_k + 0.1^j s:
-    Kraft's alpha = max(h3 / (2 (h3 - h1)), alfmin = 0.1), with their difference points too.  A
-    trial or Jacobian the search then asks for is served from the batch, so a backtracking line
-    search and the next iteration's Jacobian cost no further engine call; the (1+n)(1+K) closed
-    loops of a batch run side by side, so a call's latency barely grows.  Points are matched to
-    13 significant digits.  The iterates, the Jacobians and last_eval (taken in the search's own
-    request order) are those of the unbatched search.  trace: a list that receives each trial's
-    step ratio to its line search's first trial (diagnostics)."""
+    speculate: every new point the search asks for (a line-search trial) is scored in one batch
+    together with its n forward-difference points, so an accepted step's Jacobian costs no further
+    engine call.  Measured on the Van de Vusse run it saves nothing: SLSQP's line
+    search on these finite-difference Jacobians backtracks on most iterations, and a batch of n + 1
+    closed loops waits for its slowest one (91 s against 88 s unbatched, same endpoint).  Scoring
+    the backtracking steps ahead as well needs SLSQP's trial points bit for bit, which its caller
+    cannot reproduce; points matched to 13 digits moved the search to another endpoint.  Off by
+    default.  Points are cached by their exact value."""
     from scipy.optimize import minimize
 
     my, ny = par.my, par.ny
@@ -312,7 +309,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     asked = set()   # points the search itself has requested (MATLAB evaluates each once)
 
     def key(x):
-        return tuple(float("%.13g" % v) for v in x)
+        return tuple(np.asarray(x, dtype=float).tolist())
 
     def evals(X, spec=()):
         keys = [key(x) for x in X]
@@ -336,10 +333,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
             asked.update(new)
         return [cache[k] for k in keys]
 
-    it = {"x": None, "s": None}   # the current iterate (last Jacobian point), its first trial step
-
     def jac_F(x):
-        it["x"], it["s"] = np.array(x, dtype=float), None
         pts, h = fd_points(x)
         vals = evals(pts)
         F0 = vals[0]
@@ -349,22 +343,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     best = [np.inf, None]   # best attainment factor over the iterates / line-search points
 
     def F(x):
-        spec = []
-        if speculate and key(x) not in cache:
-            spec = fd_points(x)[0][1:]
-            if ladder and it["x"] is not None:
-                st = np.asarray(x, dtype=float) - it["x"]
-                for _ in range(ladder):
-                    st = st * 0.1
-                    p = it["x"] + st
-                    spec += fd_points(p)[0]
-        if trace is not None and it["x"] is not None and key(x) not in asked:
-            st = np.asarray(x, dtype=float) - it["x"]
-            if it["s"] is None:
-                it["s"] = st
-            nn = float(it["s"] @ it["s"])
-            trace.append(float(st @ it["s"]) / nn if nn > 0 else 0.0)
-        v = evals([x], spec=spec)[0]
+        v = evals([x], spec=fd_points(x)[0][1:] if speculate and key(x) not in cache else ())[0]
         last[0] = v
         a = float(np.max(np.abs(v - goal) / w))
         if a < best[0]:
@@ -400,7 +379,7 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
 
 # --------------------------------------------------------------------------------------------
 def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400,
-             fgam_from: str = "last_eval", stale=None, gam_speculate: bool = True, gam_ladder: int = 3):
+             fgam_from: str = "last_eval", stale=None, gam_speculate: bool = False):
     """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
     improve.  Quirks kept: Fgam = round(sum(F), 2) where F is the global GAM_fun.m:114 set on its
     LAST call (MPC_TFob.m:104), i.e. the J1 of fgoalattain's last evaluated point, not of the
@@ -414,8 +393,7 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
     delta = lam = None
     Fvns = fv
     while True:
-        x, attain, Fx, ncalls, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter, speculate=gam_speculate,
-                                                       ladder=gam_ladder)
+        x, attain, Fx, ncalls, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter, speculate=gam_speculate)
         x = x.copy()
         x[:my][par.ov_zero] = 0.0
         par.x0 = x
@@ -566,7 +544,7 @@ def stale_rows_for(yref, inK: int = 10) -> StaleRows:
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
                gam_max_iter: int = 400, lineal: bool = True, mdv=None, fgam_from: str = "last_eval",
-               stale_rows: bool = True, gam_speculate: bool = True, gam_ladder: int = 3):
+               stale_rows: bool = True, gam_speculate: bool = False):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
@@ -591,7 +569,7 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
         batch_vns = batch_vns.rows
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
                                                   gam_max_iter=gam_max_iter, fgam_from=fgam_from, stale=stale,
-                                                  gam_speculate=gam_speculate, gam_ladder=gam_ladder)
+                                                  gam_speculate=gam_speculate)
     if save_path:
         save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
     return N, Nu, delta, lam, np.array([Fvns, Fgam])

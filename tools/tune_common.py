@@ -39,24 +39,21 @@ def score_point(sc, r, N, Nu, delta, lam, w, mdv=None, vns_refs=None):
 
 def run(name, sc, r, my, ny, w, nbp, nbc, dmin, q0, w0, scale=None, mdv=None, lineal=True, out=None,
         gam_max_iter=400):
-    """Environment knobs for A/B runs: MPCT_GAM_SPECULATE=0 (one engine call per SLSQP request),
-    MPCT_GAM_LADDER=K (line-search steps scored ahead, default 3), MPCT_FGAM_FROM=returned,
-    MPCT_STALE_ROWS=0 (the round-2 quirk handling)."""
+    """Environment knobs for A/B runs: MPCT_GAM_SPECULATE=1 (each trial point scored with its
+    difference points), MPCT_FGAM_FROM=returned, MPCT_STALE_ROWS=0 (the round-2 quirk handling)."""
     from mpct.tuning import mpc_tuning
 
     out = out or os.path.join(ROOT, "gpurun_out", "%s_Tuning.mat" % name)
     t0 = time.time()
     heartbeat(t0)
-    log("%s: MPCTuning(nbp=%d, nbc=%d, w=%s, q0=%s, w0=%s, GAM max %d iterations) speculate=%s ladder=%s fgam=%s stale=%s"
+    log("%s: MPCTuning(nbp=%d, nbc=%d, w=%s, q0=%s, w0=%s, GAM max %d iterations) speculate=%s fgam=%s stale=%s"
         % (name, nbp, nbc, list(np.round(w, 6)), list(q0), list(w0), gam_max_iter,
-           os.environ.get("MPCT_GAM_SPECULATE", "1"), os.environ.get("MPCT_GAM_LADDER", "3"),
-           os.environ.get("MPCT_FGAM_FROM", "last_eval"),
+           os.environ.get("MPCT_GAM_SPECULATE", "0"), os.environ.get("MPCT_FGAM_FROM", "last_eval"),
            os.environ.get("MPCT_STALE_ROWS", "1")))
     N, Nu, delta, lam, Fob = mpc_tuning(sc, r, my=my, ny=ny, w=w, nbp=nbp, nbc=nbc, dmin=dmin, q0=q0, w0=w0,
                                         log=log, save_path=out, scale=scale, gam_max_iter=gam_max_iter,
                                         lineal=lineal, mdv=mdv,
-                                        gam_speculate=os.environ.get("MPCT_GAM_SPECULATE", "1") != "0",
-                                        gam_ladder=int(os.environ.get("MPCT_GAM_LADDER", "3")),
+                                        gam_speculate=os.environ.get("MPCT_GAM_SPECULATE", "0") == "1",
                                         fgam_from=os.environ.get("MPCT_FGAM_FROM", "last_eval"),
                                         stale_rows=os.environ.get("MPCT_STALE_ROWS", "1") != "0")
     dt = time.time() - t0
