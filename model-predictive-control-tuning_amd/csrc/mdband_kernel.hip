@@ -790,6 +790,14 @@ __global__ void __launch_bounds__(64, 1)
 #else
     iters += solve(Fc, r_t);
 #endif
+#ifdef MPCT_DEBUG_BAND_STEP
+    // diagnostic build: the QP solution and active set of simulation 0 at one step
+    if (sim == 0 && t == MPCT_DEBUG_BAND_STEP) {
+      if (lane == 0) printf("STEP %d q=%d st=%d base=%d\n", t, gis.q, st, base);
+      if (lane <= M) printf("X %d %.17e\n", lane, sxc[lane]);
+      if (lane < gis.q) printf("A %d %d %.17e\n", lane, gis.ww, gis.uw);
+    }
+#endif
     if (lane < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];

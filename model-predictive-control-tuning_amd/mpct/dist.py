@@ -25,6 +25,33 @@ def shard_indices(C: int, world: int, rank: int) -> np.ndarray:
     return rank + world * np.arange(per, dtype=np.int64)
 
 
+def band_work_estimate(N2, Nu, lam, nu=3):
+    """A-priori latency estimate of one band-mode simulation (config 3, mdband_kernel.hip): the
+    per-step output-row scan and QP grow with N2 and the QP size 3 Nu + 1, and smaller move weights
+    bind the bands more often.  Fitted on the config-3 grid's measured GI iterations and DESIGN §7's
+    flop model (log-linear, Spearman 0.98 over the grid, 0.49 within an (N2, Nu) cell):
+    N2^0.77 (nu Nu + 1)^2.07 prod(lambda)^-0.099."""
+    N2 = np.asarray(N2, dtype=float)
+    M1 = nu * np.asarray(Nu, dtype=float) + 1.0
+    lg = np.log10(np.maximum(np.abs(np.asarray(lam, dtype=float)), 1e-300)).reshape(N2.size, -1).sum(1)
+    return N2 ** 0.769 * M1 ** 2.067 * 10.0 ** (-0.0988 * lg)
+
+
+def shard_indices_keyed(work, world: int, rank: int) -> np.ndarray:
+    """Work-keyed split: candidates sorted by descending estimated work, dealt to the ranks in snake
+    order (0..W-1, W-1..0, ...), so every rank gets one candidate of every work level and the heavy
+    tail is spread evenly; each rank's candidates in ascending index order.  Pads like
+    shard_indices (indices >= C are sentinels, dealt last)."""
+    C = len(work)
+    per = -(-C // world)
+    order = np.concatenate([np.argsort(-np.asarray(work, dtype=float), kind="stable"),
+                            np.arange(C, per * world)])
+    pos = np.arange(per * world)
+    rnd, j = pos // world, pos % world
+    owner = np.where(rnd % 2 == 0, j, world - 1 - j)
+    return np.sort(order[owner == rank])
+
+
 def pad_shard(N2, Nu, delta, lam, idx):
     """The candidate arrays at ``idx`` (shard_indices), padding indices >= C with skipped
     sentinels (N2 = 0: status 8, NaN costs)."""
@@ -42,17 +69,24 @@ def pad_shard(N2, Nu, delta, lam, idx):
     return oN2, oNu, od, ol
 
 
-def gather_costs(local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather equal-size per-rank cost records [n, K] of the strided shards -> [world * n, K]
-    in candidate order: the gathered block is rank-major, row j of rank r is candidate r + j*world,
-    so one transpose of the (world, n) leading axes restores the grid's order."""
+def gather_costs(local: torch.Tensor, group=None, owners=None) -> torch.Tensor:
+    """All-gather equal-size per-rank cost records [n, K] -> [world * n, K] in candidate order.
+    Strided shards (owners None): the gathered block is rank-major, row j of rank r is candidate
+    r + j*world, so one transpose of the (world, n) leading axes restores the grid's order.  Other
+    splits: owners[r] = rank r's candidate indices (shard_indices_keyed, identical on every rank);
+    the rows are scattered to them (sentinel indices >= C land past the end)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     n = local.shape[0]
     out = torch.empty((world * n,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    return out.view((world, n) + tuple(local.shape[1:])).transpose(0, 1).reshape((world * n,) + tuple(local.shape[1:]))
+    if owners is None:
+        return out.view((world, n) + tuple(local.shape[1:])).transpose(0, 1).reshape((world * n,) + tuple(local.shape[1:]))
+    idx = torch.as_tensor(np.concatenate(owners), dtype=torch.int64, device=local.device)
+    res = torch.empty_like(out)
+    res[idx] = out
+    return res
 
 
 def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = None) -> torch.Tensor:

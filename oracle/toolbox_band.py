@@ -261,9 +261,11 @@ def kkt_residual(W, c, A, b, x, tol=1e-9):
     return rn / gn, float(s.min())
 
 
-def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
+def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl, pin=None, with_obj=False):
     """One toolbox QP: returns (x = [dU; eps], iterations).  f: free response (my*N2),
-    q: per-output tracking weight, wl: per-MV move weight (already squared / scaled)."""
+    q: per-output tracking weight, wl: per-MV move weight (already squared / scaled).
+    pin: {n: value} fixes MV n's first move du_n(0) (two extra rows), for replay checks of a
+    move taken elsewhere; with_obj: also return the objective 1/2 |W x + c|^2."""
     my, nu = sc.my, sc.nu
     M = nu * Nu
     rows, cvec = [], []
@@ -286,6 +288,10 @@ def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     b = [bb]
     e = np.zeros((1, M + 1)); e[0, M] = 1.0
     A.append(e); b.append(np.zeros(1))
+    for n, val in (pin or {}).items():
+        e = np.zeros((2, M + 1))
+        e[0, n * Nu], e[1, n * Nu] = 1.0, -1.0
+        A.append(e); b.append(np.array([val, -val]))
     for i in range(my):
         Gi = G[i * N2:(i + 1) * N2]
         fi = f[i * N2:(i + 1) * N2]
@@ -303,8 +309,12 @@ def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     viol = b - A @ x0
     need = (viol > 0) & (A[:, M] > 0)
     # hard rows (MV bounds, eps >= 0, ECR-0 outputs) hold at dU = 0 up to the rounding of u_prev
-    # (and, in replay_moves, up to the device QP's feasibility tolerance 1e-10)
-    if np.any((viol > 1e-9 * np.maximum(1.0, np.abs(b))) & ~(A[:, M] > 0)):
+    # (and, in replay_moves, up to the device QP's feasibility tolerance 1e-10); pinned rows
+    # need not
+    hard = ~(A[:, M] > 0)
+    if pin:
+        hard[Ab.shape[0] + 1:Ab.shape[0] + 1 + 2 * len(pin)] = False   # the pinned rows follow eps >= 0
+    if np.any((viol > 1e-9 * np.maximum(1.0, np.abs(b))) & hard):
         raise NotImplementedError("hard output constraint violated by the free response")
     if np.any(need):
         x0[M] = np.max(viol[need] / A[need, M]) * (1 + 1e-12)
@@ -320,6 +330,9 @@ def band_qp(sc: BandScenario, G, f, rvec, u_prev, N2, Nu, q, wl):
     res, smin = kkt_residual(Ws, c, As, bs, y)
     if res > 1e-8 or smin < -1e-9:
         raise RuntimeError("oracle QP failed its KKT check (residual %.2e, slack %.2e)" % (res, smin))
+    if with_obj:
+        x = y * dsc
+        return x, it, 0.5 * float(np.sum((W @ x + c) ** 2))
     return y * dsc, it
 
 
@@ -384,6 +397,36 @@ def closedloop_band(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, nit: i
     res = CLResult(Y, U[:nu, :nit].copy(), ys, uopt, iters, DU)
     res.eps = EPS
     return res
+
+
+def pinned_gap(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, U, t: int):
+    """Replay check of the move an applied MV trajectory U (nu x nit) took at step t, judged by
+    the QP's objective instead of the moves: the toolbox QP at the state U reached, solved free
+    and with the first moves pinned to U's (du_n(0) = U[n, t] - U[n, t-1]).  Returns (J_free,
+    J_pinned, du_oracle).  At steps where the soft-band slack dominates the cost by orders of
+    magnitude the optimum is flat along the moves: the pinned QP then reaches the free optimum
+    to ~1e-12 relative although the moves differ at 1e-6."""
+    my, nu, nd, nin = sc.my, sc.nu, sc.nd, sc.nin
+    nit = U.shape[1]
+    r = np.asarray(r, dtype=float).reshape(my, nit)
+    v = np.asarray(v, dtype=float).reshape(nd, nit)
+    delta = np.abs(np.asarray(delta, dtype=float))
+    lam = np.abs(np.asarray(lam, dtype=float))
+    wq = (delta / sc.sy) ** 2 if sc.weights_squared else delta / sc.sy
+    wl = (lam / sc.su) ** 2 if sc.weights_squared else lam / sc.su
+    ba = sc.ba()
+    G = dyn_matrix(step_table(sc, N2 + 2), nu, N2, Nu)
+    u_prev = U[:, t - 1] if t > 0 else np.zeros(nu)
+    Uf = np.zeros((nin, t + N2 + 1))
+    Uf[:nu, :t] = U[:, :t]
+    Uf[nu:, :t] = v[:, :t]
+    Uf[:nu, t:] = u_prev[:, None]
+    Uf[nu:, t:] = v[:, t][:, None]
+    f = simulate(ba, Uf, t + N2 + 1)[:, t + 1:].reshape(-1)
+    x, _, J0 = band_qp(sc, G, f, r[:, t], u_prev, N2, Nu, wq, wl, with_obj=True)
+    pin = {n: float(U[n, t] - u_prev[n]) for n in range(nu)}
+    _, _, J1 = band_qp(sc, G, f, r[:, t], u_prev, N2, Nu, wq, wl, pin=pin, with_obj=True)
+    return J0, J1, np.array([x[n * Nu] for n in range(nu)])
 
 
 def replay_moves(sc: BandScenario, r, v, N2: int, Nu: int, delta, lam, U, T=None):

@@ -96,3 +96,35 @@ def test_config3_fixture_reproduces(shell):
     o = cb.eval(N2[idx], Nu[idx], D[idx], L[idx], r[None], v[None], threads=4)
     np.testing.assert_allclose(o["J1"], d["J1_strat"][pick], rtol=1e-12)
     np.testing.assert_allclose(o["J1"] @ SHELL7_W, d["F_full"][idx], rtol=1e-12)
+
+
+def test_pinned_gap_judges_moves_by_cost(shell):
+    """toolbox_band.pinned_gap (the objective form of the replay check): the oracle's own moves
+    attain its optimum; on Shell 7x5 after the disturbance enters, a move pushed 5 % off the
+    optimum changes the cost by ~1e-13 only (the band slack dominates: the flat optimum of
+    DESIGN §11); with tracking weights (WoodBerry) the same push costs visibly more."""
+    from oracle.cband import CBand
+    from oracle.scenarios import woodberry_toolbox
+    from oracle.toolbox_band import pinned_gap
+
+    sc, r, v, yref, fx, cb = shell
+    N2, Nu, lm = 16, 3, np.array([0.1, 0.03, 2.0])
+    o = cb.eval([N2], [Nu], np.zeros((1, 7)), lm[None], r[None], v[None], want_traj=True)
+    U = o["u"][0]
+    for t in (5, 25, 60):
+        J0, J1, du = pinned_gap(sc, r, v, N2, Nu, np.zeros(7), lm, U, t)
+        assert abs(J1 - J0) <= 1e-9 * J0
+        np.testing.assert_allclose(du, U[:, t] - U[:, t - 1], rtol=1e-7, atol=1e-15)
+    Up = U.copy()
+    Up[0, 25:] += 0.05 * abs(U[0, 25] - U[0, 24])
+    J0, J1, _ = pinned_gap(sc, r, v, N2, Nu, np.zeros(7), lm, Up, 25)
+    assert 0 <= J1 - J0 < 1e-9 * J0                          # flat along the moves
+    wsc, wr, wv, wy = woodberry_toolbox()
+    d, lw = np.array([1.0, 0.5]), np.array([0.1, 0.2])
+    ow = CBand(wsc, 400, wy).eval([12], [3], d[None], lw[None], wr[None], wv[None], want_traj=True)
+    Uw = ow["u"][0].copy()
+    J0, J1, _ = pinned_gap(wsc, wr, wv, 12, 3, d, lw, Uw, 20)
+    assert abs(J1 - J0) <= 1e-9 * J0
+    Uw[0, 20:] += 0.05 * abs(Uw[0, 20] - Uw[0, 19])
+    J0, J1, _ = pinned_gap(wsc, wr, wv, 12, 3, d, lw, Uw, 20)
+    assert J1 - J0 > 1e-6 * J0

@@ -34,17 +34,21 @@ def _costs(N2, Nu, d, l):
     return out
 
 
-def _worker(rank, world, port, C, q):
+def _worker(rank, world, port, C, q, keyed=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_indices
+        from mpct.dist import gather_costs, pad_shard, rank_candidates, shard_indices, shard_indices_keyed
         from mpct.scenarios import candidate_grid
 
         N2, Nu, d, l = candidate_grid(C)
-        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, shard_indices(C, world, rank))
+        owners = None
+        if keyed:   # any work key: the weight ratio stands in for config 3's latency estimate
+            w = d.max(1) / l.min(1)
+            owners = [shard_indices_keyed(w, world, k) for k in range(world)]
+        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, owners[rank] if keyed else shard_indices(C, world, rank))
         local = torch.from_numpy(_costs(sN2, sNu, sd, sl))
-        g = gather_costs(local)
+        g = gather_costs(local, owners=owners)
         w = torch.tensor([0.05, 0.40, 0.55], dtype=torch.float64)
         order = rank_candidates(g, w, C)
         q.put((rank, g.numpy(), order.numpy()))
@@ -52,15 +56,15 @@ def _worker(rank, world, port, C, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("C", [12, 11])
-def test_two_rank_gather_and_rank(built, C):
+@pytest.mark.parametrize("C,keyed", [(12, False), (11, False), (11, True)])
+def test_two_rank_gather_and_rank(built, C, keyed):
     from mpct.scenarios import candidate_grid
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, C, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, C, q, keyed)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=300) for _ in range(world)]

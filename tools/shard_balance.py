@@ -1,8 +1,9 @@
 """Per-shard time of the 8-rank splits on one GPU: for config 3 (the 65,536
 Shell 7x5 grid, cell-ordered) and config 4 (10,000 WoodBerry DTC candidates x 32 draws), each of
-the 8 shards of the contiguous (round 2) and strided (round 3, mpct.dist.shard_indices) splits is
-scored alone on cuda:0 and timed with HIP events; max/mean shard time predicts the 8-GPU
-efficiency loss from imbalance.  Usage: python tools/shard_balance.py [--out FILE]"""
+the 8 shards of the contiguous (round 2), strided (mpct.dist.shard_indices) and, for config 3,
+work-keyed (mpct.dist.shard_indices_keyed) splits is scored alone on cuda:0 and timed with HIP
+events (median of 3); max/mean shard time predicts the 8-GPU efficiency loss from imbalance.
+Usage: python tools/shard_balance.py [--out FILE]"""
 import argparse
 import json
 import os
@@ -14,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "model-predictive-control-tuning_amd")]
 import torch  # noqa: E402
 
-from mpct.dist import pad_shard, shard_indices  # noqa: E402
+from mpct.dist import band_work_estimate, pad_shard, shard_indices, shard_indices_keyed  # noqa: E402
 from mpct.engine import eval_batch_device  # noqa: E402
 
 
@@ -30,7 +31,7 @@ def workload(name):
     return sc, config4_candidates(10000), r, v, 32
 
 
-def time_shard(sc, cand, refs, v, nref, idx, reps=2):
+def time_shard(sc, cand, refs, v, nref, idx, reps=3):
     dev = torch.device("cuda:0")
     N2, Nu, d, l = pad_shard(*cand, idx)
     t = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in dict(N2=N2, Nu=Nu, d=d, l=l, r=refs).items()}
@@ -49,7 +50,7 @@ def time_shard(sc, cand, refs, v, nref, idx, reps=2):
         torch.cuda.synchronize()
         if k:
             ms.append(e0.elapsed_time(e1))
-    return min(ms)
+    return float(np.median(ms))
 
 
 def main():
@@ -64,10 +65,16 @@ def main():
         C = len(cand[0])
         per = -(-C // W)
         res = {}
-        for split in ("contiguous", "strided"):
+        splits = ("contiguous", "strided", "keyed") if name == "shell7x5" else ("contiguous", "strided")
+        for split in splits:
             times = []
             for rk in range(W):
-                idx = np.arange(rk * per, (rk + 1) * per) if split == "contiguous" else shard_indices(C, W, rk)
+                if split == "contiguous":
+                    idx = np.arange(rk * per, (rk + 1) * per)
+                elif split == "strided":
+                    idx = shard_indices(C, W, rk)
+                else:
+                    idx = shard_indices_keyed(band_work_estimate(cand[0], cand[1], cand[3]), W, rk)
                 times.append(time_shard(sc, cand, refs, v, nref, idx))
                 print(name, split, rk, "%.1f ms" % times[-1], flush=True)
             res[split] = dict(shard_ms=times, max_over_mean=max(times) / float(np.mean(times)))
