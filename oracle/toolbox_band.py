@@ -257,7 +257,9 @@ def kkt_residual(W, c, A, b, x, tol=1e-9):
     gn = max(1.0, float(np.linalg.norm(grad)))
     if not act.any():
         return float(np.linalg.norm(grad)) / gn, float(s.min(initial=np.inf))
-    _, rn = nnls(A[act].T, grad)
+    # many near-parallel active band rows (the cold QP where the disturbance enters) need more
+    # than scipy's default 3n Lawson-Hanson iterations
+    _, rn = nnls(A[act].T, grad, maxiter=max(1000, 50 * int(act.sum())))
     return rn / gn, float(s.min())
 
 
