@@ -82,7 +82,11 @@ template <int MAXM>
 __device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
                                              bool row) {
   const int lane = qp_lane();
+  // not unrolled: the x8 unroll hoists eight strided LDS pointers, the one VGPR over the 3-wave
+  // budget of gpc_closed_loop_kernel<16>, spilled to scratch (~1 MiB of write-backs per metric
+  // launch); the rebuild runs once per 32 updates so the loop overhead is noise
   if (row)
+#pragma unroll 1
     for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
   S.nrot = 0;
   S.jinit = true;

@@ -25,9 +25,6 @@
 #include "gi_core.h"
 #include "gpc_qp.h"
 
-#ifndef MPCT_STAGE_RESULTS
-#define MPCT_STAGE_RESULTS 1  // ordered launches write their cost records XCD-major, then gather (DevResult::stage)
-#endif
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
                              // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
@@ -141,16 +138,17 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   auto put_record = [&](double j1v, double j21v, double j22v, double jnuv, int status, long long itv)
                         __attribute__((always_inline)) {
     if (out.stage) {
-      double* row = out.stage + xcd_row(slot, C * nref) * stage_width(my, nu);
+      const StageRow& R = out.srow;
+      double* row = out.stage + xcd_row(slot, C * nref) * R.w;
       if (lane < my) {
-        row[lane] = j1v;
-        row[my + lane] = j21v;
-        row[2 * my + lane] = j22v;
+        if (R.j1 >= 0) row[R.j1 + lane] = j1v;
+        if (R.j21 >= 0) row[R.j21 + lane] = j21v;
+        if (R.j22 >= 0) row[R.j22 + lane] = j22v;
       }
-      if (lane < nu) row[3 * my + lane] = jnuv;
+      if (lane < nu && R.jnu >= 0) row[R.jnu + lane] = jnuv;
       if (lane == 0) {
-        row[3 * my + nu] = (double)status;
-        row[3 * my + nu + 1] = (double)itv;
+        if (R.st >= 0) row[R.st] = (double)status;
+        if (R.it >= 0) row[R.it] = (double)itv;
       }
       return;
     }
@@ -667,9 +665,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #include "work_order.h"
 #include "launch_fan.h"
 
-#ifndef MPCT_STAGE_RESULTS
-#define MPCT_STAGE_RESULTS 1  // ordered launches write their cost records XCD-major, then gather (DevResult::stage)
-#endif
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
                              // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
@@ -750,8 +745,9 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
   // ordered launches stage their cost records XCD-major and gather them into the caller's order
   // afterwards (DevResult::stage): full-line writes instead of 24-B pieces from every L2
   DevResult lo = out;
-  if (perm && MPCT_STAGE_RESULTS) {
-    const int rs = order_stage(*wo, C * nref, sc.my, sc.nu, &lo.stage, err);
+  if (perm) {
+    lo.srow = stage_row(out, sc.my, sc.nu);
+    const int rs = lo.srow.w ? order_stage(*wo, C * nref, lo.srow.w, &lo.stage, err) : 0;
     if (rs) return rs;
   }
   int rc = 0;
@@ -771,7 +767,7 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     ++k;
   }
   fs.join();
-  if (rc == 0 && lo.stage) rc = unpermute_results(*wo, C, nref, sc.my, sc.nu, out, stream, err);
+  if (rc == 0 && lo.stage) rc = unpermute_results(*wo, C, nref, sc.my, sc.nu, lo.srow, out, stream, err);
   if (perm) order_mark_used(*wo, stream);
   return rc;
 }

@@ -105,19 +105,26 @@ struct DevOpts {
   double feas_tol;
 };
 
+// staging row of an ordered launch: the fields the caller asked for, in the order
+// J1 [my] | j21 [my] | j22 [my] | Jnu [nu] | status | qp_iters (one double each); -1 = not staged
+struct StageRow {
+  int w, j1, j21, j22, jnu, st, it;
+};
+
 struct DevResult {
   double *J1, *j21, *j22, *Jnu;
   int32_t* status;
   int64_t* qp_iters;
   double *y, *u, *ys, *uopt;
   unsigned long long* prof;  // diagnostic builds only (-DMPCT_PROFILE): [sim][8] cycle sums
-  // ordered launches: the cost record of workgroup slot k goes to staging row xcd_row(k) instead
-  // of the caller's arrays, and unpermute_results gathers it back into the caller's order.  The
-  // workgroups of a launch are dealt to the 8 XCDs round robin, so XCD x's slots fill one
-  // contiguous block of rows and every 128-B line is written from one L2; written straight to the
-  // caller's (permuted) index, a line collects 24-B pieces from up to 8 L2s and each writes back
-  // its partial copy (5x the result bytes in WRITE_SIZE, profiles/r02m_pmc.json).
+  // ordered launches: the cost record of workgroup slot k goes to staging row xcd_row(k) (layout
+  // srow) instead of the caller's arrays, and unpermute_results gathers it back into the caller's
+  // order.  The workgroups of a launch are dealt to the 8 XCDs round robin, so XCD x's slots fill
+  // one contiguous block of rows and every 128-B line is written whole from one L2; written
+  // straight to the caller's (permuted) index, a line collects 24-B pieces from up to 8 L2s and
+  // each writes back its partial copy (2.6x the result bytes in WRITE_SIZE).
   double* stage = nullptr;
+  StageRow srow = {0, -1, -1, -1, -1, -1, -1};
 };
 
 constexpr int kXcds = 8;
@@ -125,8 +132,22 @@ constexpr int kXcds = 8;
 __host__ __device__ inline long long xcd_row(long long k, long long S) {
   return (k % kXcds) * ((S + kXcds - 1) / kXcds) + k / kXcds;
 }
-// staging row layout: J1 [my] | j21 [my] | j22 [my] | Jnu [nu] | status | qp_iters, padded even
-__host__ __device__ inline int stage_width(int my, int nu) { return (3 * my + nu + 2 + 1) & ~1; }
+inline StageRow stage_row(const DevResult& o, int my, int nu) {
+  StageRow r = {0, -1, -1, -1, -1, -1, -1};
+  auto put = [&r](bool on, int n, int& f) {
+    if (on) {
+      f = r.w;
+      r.w += n;
+    }
+  };
+  put(o.J1 != nullptr, my, r.j1);
+  put(o.j21 != nullptr, my, r.j21);
+  put(o.j22 != nullptr, my, r.j22);
+  put(o.Jnu != nullptr, nu, r.jnu);
+  put(o.status != nullptr, 1, r.st);
+  put(o.qp_iters != nullptr, 1, r.it);
+  return r;
+}
 
 // section ids of the diagnostic in-kernel stamps
 enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,

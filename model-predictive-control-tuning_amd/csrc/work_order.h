@@ -37,9 +37,9 @@ int rank_device(const double* costs, long long C, int k, const double* w, int* p
 // staging rows for the cost records of an ordered launch of S simulations (DevResult::stage), and
 // the gather of those rows back into the caller's order (one thread per simulation, contiguous
 // writes); enqueue the gather after every launch of the batch
-int order_stage(WorkOrder& wo, long long S, int my, int nu, double** stage, std::string* err);
-int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const DevResult& out,
-                      hipStream_t stream, std::string* err);
+int order_stage(WorkOrder& wo, long long S, int width, double** stage, std::string* err);
+int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const StageRow& R,
+                      const DevResult& out, hipStream_t stream, std::string* err);
 
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);

@@ -349,8 +349,8 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   return 0;
 }
 
-int order_stage(WorkOrder& wo, long long S, int my, int nu, double** stage, std::string* err) {
-  const size_t need = (size_t)kXcds * ((S + kXcds - 1) / kXcds) * stage_width(my, nu) * sizeof(double);
+int order_stage(WorkOrder& wo, long long S, int width, double** stage, std::string* err) {
+  const size_t need = (size_t)kXcds * ((S + kXcds - 1) / kXcds) * width * sizeof(double);
   if (need > wo.stage_bytes) {
     if (wo.stage) (void)hipFree(wo.stage);
     wo.stage = nullptr;
@@ -367,29 +367,29 @@ int order_stage(WorkOrder& wo, long long S, int my, int nu, double** stage, std:
 
 // thread s = c*nref + k of the caller's order reads the staging row of slot inv[c]*nref + k
 __global__ void unpermute_kernel(const double* __restrict__ stage, const int* __restrict__ inv, long long C,
-                                 int nref, int my, int nu, DevResult out) {
+                                 int nref, int my, int nu, StageRow R, DevResult out) {
   const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long S = C * nref;
   if (s >= S) return;
   const long long c = s / nref;
   const long long slot = (long long)inv[c] * nref + (s - c * nref);
-  const double* row = stage + xcd_row(slot, S) * stage_width(my, nu);
+  const double* row = stage + xcd_row(slot, S) * R.w;
   for (int i = 0; i < my; ++i) {
-    if (out.J1) out.J1[s * my + i] = row[i];
-    if (out.j21) out.j21[s * my + i] = row[my + i];
-    if (out.j22) out.j22[s * my + i] = row[2 * my + i];
+    if (R.j1 >= 0) out.J1[s * my + i] = row[R.j1 + i];
+    if (R.j21 >= 0) out.j21[s * my + i] = row[R.j21 + i];
+    if (R.j22 >= 0) out.j22[s * my + i] = row[R.j22 + i];
   }
-  if (out.Jnu)
-    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = row[3 * my + i];
-  if (out.status) out.status[s] = (int)row[3 * my + nu];
-  if (out.qp_iters) out.qp_iters[s] = (long long)row[3 * my + nu + 1];
+  if (R.jnu >= 0)
+    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = row[R.jnu + i];
+  if (R.st >= 0) out.status[s] = (int)row[R.st];
+  if (R.it >= 0) out.qp_iters[s] = (long long)row[R.it];
 }
 
-int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const DevResult& out,
-                      hipStream_t stream, std::string* err) {
+int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const StageRow& R,
+                      const DevResult& out, hipStream_t stream, std::string* err) {
   const long long S = C * nref;
   hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream,
-                     static_cast<const double*>(wo.stage), wo.inv, C, nref, my, nu, out);
+                     static_cast<const double*>(wo.stage), wo.inv, C, nref, my, nu, R, out);
   if (hipGetLastError() != hipSuccess) {
     *err = "unpermute_results launch failed";
     return -3;
