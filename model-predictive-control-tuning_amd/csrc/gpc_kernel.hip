@@ -32,12 +32,6 @@
 #ifndef MPCT_WAVES32
 #define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
 #endif
-#ifndef MPCT_REG_DU
-#define MPCT_REG_DU 0  // past-control registers in VGPRs (else shifted in LDS; 0 measured faster)
-#endif
-#ifndef MPCT_REG_Y
-#define MPCT_REG_Y 0   // y backward-difference histories in VGPRs (else in LDS; 0 measured faster)
-#endif
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
 #endif
@@ -452,9 +446,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const double* ea = spla + ee * sc.pl_maxa;
   double* eyh = syeh + lane * kYeHist;
   const double* eur = sur + (ecopy * nin + ej) * kURing;
-  // register-resident per-lane state (regpath): plant entry taps / denominator / output history,
-  // output y(t-1) and its backward differences, MV past-control register
-  double bt[kRegB], at[kRegA], yh[kRegA], yd[kRegY], duh[kRegDu];
+  // register-resident per-lane state (regpath): plant entry taps / denominator / output history
+  double bt[kRegB], at[kRegA], yh[kRegA];
 #pragma unroll
   for (int k = 0; k < kRegB; ++k) bt[k] = (is_entry && k < e_nb - e_off) ? eb[e_off + k] : 0.0;
 #pragma unroll
@@ -462,10 +455,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     at[k] = (is_entry && k + 1 < e_na) ? ea[k + 1] : 0.0;
     yh[k] = 0.0;
   }
-#pragma unroll
-  for (int k = 0; k < kRegY; ++k) yd[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < kRegDu; ++k) duh[k] = 0.0;
   const bool regpath = sc.regpath != 0;
   // prefetched per-output signals
   double r_t = 0.0, yr_t = 0.0;
@@ -479,17 +468,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
-      if (regpath && MPCT_REG_DU) {  // past-control register in registers, written out whole
-#pragma unroll
-        for (int k = kRegDu - 1; k > 0; --k) duh[k] = duh[k - 1];
-        duh[0] = du;
-#pragma unroll
-        for (int k = 0; k < kRegDu; ++k)
-          if (k < dum_n) sx[upoff_n + k] = duh[k];
-      } else {
-        for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
-        sx[upoff_n] = du;
-      }
+      // past-control register shifted in LDS (kept in VGPRs it measured slower: register pressure)
+      for (int k = dum_n - 1; k > 0; --k) sx[upoff_n + k] = sx[upoff_n + k - 1];
+      sx[upoff_n] = du;
       sur[n * kURing + (t & (kURing - 1))] = un;
       if ((EXT && o.want_traj)) {
         if (out.u) out.u[(sim * nu + n) * nit + t] = un;
@@ -597,30 +578,16 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         ym = ygz + yfr;
       }
       // state: [y - r, nabla y, ..., nabla^na y]; nabla^k y(t) = nabla^{k-1} y(t) - nabla^{k-1} y(t-1)
-      if (regpath && MPCT_REG_Y) {  // yd = [y(t-1), nabla y(t-1), ...] in registers
-        double cur = ym, prev = yd[0];
-#pragma unroll
-        for (int k = 1; k < kRegY; ++k) {
-          if (k < nyh_i) {
-            const double nk = cur - prev;
-            prev = yd[k];
-            yd[k] = nk;
-            cur = nk;
-            sx[yoff_i + k] = nk;
-          }
-        }
-        yd[0] = ym;
-      } else {
-        double cur = ym, prev = syprev[i];
-        for (int k = 1; k < nyh_i; ++k) {
-          const double old = sx[yoff_i + k];
-          const double nk = cur - prev;
-          sx[yoff_i + k] = nk;
-          cur = nk;
-          prev = old;
-        }
-        syprev[i] = ym;
+      // backward differences shifted in LDS (kept in VGPRs they measured slower)
+      double cur = ym, prev = syprev[i];
+      for (int k = 1; k < nyh_i; ++k) {
+        const double old = sx[yoff_i + k];
+        const double nk = cur - prev;
+        sx[yoff_i + k] = nk;
+        cur = nk;
+        prev = old;
       }
+      syprev[i] = ym;
       sx[yoff_i] = ym - r_t;
       const double e1 = y - yr_t;
       j1 += e1 * e1;
@@ -665,10 +632,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #include "work_order.h"
 #include "launch_fan.h"
 
-#ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
-                             // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
-#endif
 namespace mpct {
 
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {

@@ -29,8 +29,8 @@ constexpr int kMaxDum = 16;    // longest past-control register per MV (deltaUFr
 // register-resident per-lane state (DevScenario::regpath; larger scenarios use the LDS path)
 constexpr int kRegB = 4;       // nonzero numerator taps per plant entry
 constexpr int kRegA = 4;       // denominator coefficients a_1.. per plant entry
-constexpr int kRegDu = 8;      // past-control register length per MV
-constexpr int kRegY = 6;       // y history (difference basis) length per output
+constexpr int kRegDu = 8;      // past-control register length per MV (regpath eligibility)
+constexpr int kRegY = 6;       // y history (difference basis) length per output (regpath eligibility)
 constexpr int kWave = 64;
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)

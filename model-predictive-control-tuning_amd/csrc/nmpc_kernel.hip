@@ -84,13 +84,7 @@ template <bool TAN>
 __device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const double u[2], const double xd[3],
                                         const double ud[2], double f[3], double fd[3]) {
   const double ca = x[0], cb = x[1], T = x[2];
-#if MPCT_EXP_RHS == 1  // ablation: one more exp in series on the rhs chain (value unchanged)
-  const double th = T + 273.15 + 0.0 * exp(T * 1e-3);
-#elif MPCT_EXP_RHS == 2  // ablation: one more division in series (value unchanged)
-  const double th = T + 273.15 + 0.0 * (1.0 / T);
-#else
   const double th = T + 273.15;
-#endif
 #if MPCT_RHS_FAST >= 1
   const double ith = rcp_nr(th);
 #else
