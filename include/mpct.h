@@ -314,7 +314,8 @@ int32_t mpct_rank_device(const double* costs, int64_t C, int32_t k, const double
  * No device needed (tests pin the instance a benchmark times). */
 int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts* opts, char* buf, int32_t cap);
 
-/* Bytes of dynamic LDS one simulation's workgroup uses for this scenario at (N2, Nu); <0 on
+/* Bytes of dynamic LDS one simulation's workgroup uses for this scenario at (N2, Nu) with the
+ * open-loop leg / trajectories on (the cost-only instance of a linear scenario needs less); <0 on
  * error.  Lets a host check occupancy before launching. */
 int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu);
 

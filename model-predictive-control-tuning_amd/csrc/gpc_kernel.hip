@@ -43,11 +43,15 @@ struct LdsLayout {
       mza, frb, fra, total;
 };
 
-// LDS layout of one simulation; [x, plb) holds the state and every history (zeroed at start)
-__host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
+// LDS layout of one simulation; [x, plb) holds the state and every history (zeroed at start).
+// ext: the EXT instance, whose open-loop leg needs a second copy of the plant state and Uopt; the
+// cost-only instance leaves them out (13,440 -> 12,472 B at Shell 3x3: 12 instead of 11
+// workgroups per CU at the 512-B LDS allocation granularity)
+__host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bool ext) {
   const int nx = sc.nx, nu = sc.nu, nin = sc.nin, ne = sc.ne, my = sc.my;
   const int nmz = sc.dtc ? 2 * my * nu : 0;  // DTC predictor model entries (Pz, Gz)
   const int nfr = sc.dtc ? my : 0;           // DTC robustness filters
+  const int ncp = ext ? 2 : 1;               // plant copies: closed loop (+ open loop)
   LdsLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
@@ -63,10 +67,10 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   L.xc = take(M);
   L.uprev = take(nu);
   L.yprev = take(my);
-  L.ucum = take(M);
-  L.ye = take(2 * ne);
-  L.yeh = take(sc.regpath ? 0 : 2 * ne * kYeHist);  // register-resident histories need none
-  L.uring = take(2 * nin * kURing);
+  L.ucum = take(ext ? M : 0);
+  L.ye = take(ncp * ne);
+  L.yeh = take(sc.regpath ? 0 : ncp * ne * kYeHist);  // register-resident histories need none
+  L.uring = take(ncp * nin * kURing);
   L.mzh = take(nmz * kYeHist);   // DTC: model entry output histories
   L.smz = take(nmz);             // DTC: model entry outputs of the step
   L.frh = take(nfr * 2 * kYeHist);  // DTC: filter input (eM) and output histories
@@ -76,6 +80,9 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M) {
   L.mza = take(nmz * (sc.dtc ? sc.mz_maxa : 0));
   L.frb = take(nfr * (sc.dtc ? sc.fr_max : 0));
   L.fra = take(nfr * (sc.dtc ? sc.fr_max : 0));
+#ifdef MPCT_EXP_LDS_PAD
+  take(MPCT_EXP_LDS_PAD);  // occupancy probes: doubles of padding
+#endif
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -127,6 +134,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   unsigned long long pacc[PROF_N] = {};
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef MPCT_TIMELINE
+  // diagnostic build: when this workgroup ran and where (tools/diag/timeline.py)
+  const unsigned long long tl_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // the cost record: caller's arrays at `sim`, or staging row xcd_row(slot) (ordered launches)
   auto put_record = [&](double j1v, double j21v, double j22v, double jnuv, int status, long long itv)
@@ -167,7 +178,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     return;
   }
   if (M <= mlo || M > MAXM) return;  // another QP-size class launch simulates it
-  const LdsLayout L = lds_layout(sc, M);
+  const LdsLayout L = lds_layout(sc, M, EXT);
   const int nxp = (nx + 1) & ~1;  // padded row length of A (x[nx] and the pad column are 0)
   double* sRi = lds + L.rinv;
   double* sA = lds + L.A;
@@ -202,10 +213,16 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const double* lm = lambdav + c * nu;
   lds_sync();
 
-  // QR of W = [Q^1/2 G; Lambda^1/2] by row-streamed Givens rotations carrying V = [Q^1/2 Phi; 0]
-  // (lane l < M owns column l of R, lane l >= M a column of T = Q1'V; rotation k decided by lane
-  // k, broadcast with v_readlane).  When M + nx > 64 the V columns are processed in passes of
-  // 64 - M; every pass recomputes the same rotations (bitwise identical R), so T is exact.
+  // QR of W = [Q^1/2 G; Lambda^1/2] carrying V = [Q^1/2 Phi; 0], streaming W's rows in blocks of
+  // kHB (lane l < M owns column l of R, lane l >= M a column of T = Q1'V).  R's row k absorbs a
+  // block by one Householder reflection that annihilates the block's column k: x = [R_kk; w_.k],
+  // R_kk <- ||x|| (kept positive), v = x - ||x|| e1 with v_0 = -sigma / (R_kk + ||x||) (sigma =
+  // ||w_.k||^2: no cancellation), H = I - beta v v', beta = -1 / (||x|| v_0).  The reflection is
+  // decided by lane k and broadcast with v_readlane; per block of 8 rows it issues about half the
+  // VALU of 8 Givens rotations (one rsq / rcp chain per column instead of one per row).  When
+  // M + nx > 64 the V columns are processed in passes of 64 - M; every pass recomputes the same
+  // reflections (bitwise identical R), so T is exact.
+  constexpr int kHB = 8;
   const int vper = kWave - M;  // V columns per pass (host guarantees M < 64)
   const int npass = (nx + vper - 1) / vper;
   double rcol[MAXM];
@@ -213,6 +230,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   if (lane < M) {
     gn = lane / Nu;
     gc = lane - gn * Nu;
+  }
+  double sqv = 0.0;  // lane i < my: the output weight's square root (broadcast per row)
+  if (lane < my) {
+    const double di = fabs(dl[lane]);
+    sqv = sc.wsq ? di : sqrt(di);
   }
   double* sR = lds + L.jt;  // R (upper, row-major) parks in J's region until the QP starts
   for (int pass = 0; pass < npass; ++pass) {
@@ -227,55 +249,72 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #pragma unroll
       for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? wl0 : 0.0;
     }
-    // lane's entry of the weighted row g = i*N2 + r of [Q^1/2 G | Q^1/2 Phi]
-    auto rowval = [&](int g) __attribute__((always_inline)) -> double {
-      const int i = g / N2, r = g - i * N2;
-      const double di = fabs(dl[i]);
-      const double sqi = sc.wsq ? di : sqrt(di);
+    // lane's entry of the next weighted row (output fi, prediction step fr) of
+    // [Q^1/2 G | Q^1/2 Phi]; zero rows past the end pad the last block
+    int fi = 0, fr = 0;
+    auto fetch = [&]() __attribute__((always_inline)) -> double {
       double v = 0.0;
-      if (lane < M) {
-        const int tt = sc.n1[i] + r - gc;
-        v = tt >= 0 ? sc.step[(i * nu + gn) * sc.tlen + tt] : 0.0;  // prologue only: global (L2)
-      } else if (vlane) {
-        v = sc.phi[(long long)(i * sc.n2max + r) * nx + vc];
+      if (fi < my) {
+        if (lane < M) {
+          const int tt = sc.n1[fi] + fr - gc;
+          v = tt >= 0 ? sc.step[(fi * nu + gn) * sc.tlen + tt] : 0.0;  // prologue only: global (L2)
+        } else if (vlane) {
+          v = sc.phi[(long long)(fi * sc.n2max + fr) * nx + vc];
+        }
+        v *= bcast(sqv, fi);
+        if (++fr == N2) {
+          fr = 0;
+          ++fi;
+        }
       }
-      return v * sqi;
+      return v;
     };
-    // Givens rotation of row w against R's row k (decided by lane k, uniform); identity when
-    // the row's entry is already zero.  1/rho by v_rsq_f64 and two Newton steps.
-    auto rotate = [&](double& w, int k) __attribute__((always_inline)) {
-      const double b = bcast(w, k);
-      const double a = bcast(rcol[k], k);
-      const double x = a * a + b * b;
-      double ri = __builtin_amdgcn_rsq(x);
-      const double h = 0.5 * x;
-      ri = ri * fma(-h * ri, ri, 1.5);
-      ri = ri * fma(-h * ri, ri, 1.5);
-      const bool nz = b != 0.0;
-      const double cs = nz ? a * ri : 1.0, sn = nz ? b * ri : 0.0;
-      const double rk = rcol[k];
-      rcol[k] = cs * rk + sn * w;
-      w = -sn * rk + cs * w;
-    };
-    // two rows in flight, skewed by one column (independent latency chains interleave)
-    const int P = my * N2;
-    int g = 0;
-    double n0 = P > 0 ? rowval(0) : 0.0, n1v = P > 1 ? rowval(1) : 0.0;  // prefetched pair
-    for (; g + 1 < P; g += 2) {
-      double w0 = n0, w1 = n1v;
-      if (g + 2 < P) n0 = rowval(g + 2);
-      if (g + 3 < P) n1v = rowval(g + 3);
+    auto reflect = [&](double (&w)[kHB], int k) __attribute__((always_inline)) {
+      double wk[kHB];
+      double sg0 = 0.0, sg1 = 0.0;
 #pragma unroll
-      for (int k = 0; k <= MAXM; ++k) {
-        if (k < M) rotate(w0, k);
-        if (k >= 1 && k - 1 < M) rotate(w1, k - 1);
+      for (int i = 0; i < kHB; ++i) {
+        wk[i] = bcast(w[i], k);
+        if (i & 1) sg1 = fma(wk[i], wk[i], sg1);
+        else sg0 = fma(wk[i], wk[i], sg0);
       }
-    }
-    if (g < P) {
-      double w0 = n0;
+      const double sig = sg0 + sg1;
+      if (sig == 0.0) return;  // uniform: the block's column k is already zero
+      const double x0 = bcast(rcol[k], k);
+      const double rn = rsq_nr(fma(x0, x0, sig));  // 1 / ||x||
+      const double rs = rcp_nr(sig);
+      const double n = fma(x0, x0, sig) * rn;
+      const double xpn = x0 + n;
+      const double v0 = -sig * rcp_nr(xpn);
+      const double beta = rn * xpn * rs;  // -1 / (||x|| v_0)
+      double s0 = v0 * rcol[k], s1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < kHB; ++i) {
+        if (i & 1) s1 = fma(wk[i], w[i], s1);
+        else s0 = fma(wk[i], w[i], s0);
+      }
+      const double f = beta * (s0 + s1);
+      const bool own = lane == k;
+      rcol[k] = own ? n : fma(-f, v0, rcol[k]);
+#pragma unroll
+      for (int i = 0; i < kHB; ++i) w[i] = own ? 0.0 : fma(-f, wk[i], w[i]);
+    };
+    const int P = my * N2;
+    const int nblk = (P + kHB - 1) / kHB;
+    double nb[kHB];
+#pragma unroll
+    for (int i = 0; i < kHB; ++i) nb[i] = fetch();
+    for (int blk = 0; blk < nblk; ++blk) {
+      double w[kHB];
+#pragma unroll
+      for (int i = 0; i < kHB; ++i) w[i] = nb[i];
+      if (blk + 1 < nblk) {  // prefetch the next block (L2 latency under the reflections)
+#pragma unroll
+        for (int i = 0; i < kHB; ++i) nb[i] = fetch();
+      }
 #pragma unroll
       for (int k = 0; k < MAXM; ++k)
-        if (k < M) rotate(w0, k);
+        if (k < M) reflect(w, k);
     }
     if (pass == 0) {  // R to LDS; singular R -> status
       lds_sync();
@@ -615,6 +654,17 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   if (lane == 0 && out.prof)
     for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
 #endif
+#ifdef MPCT_TIMELINE
+  if (lane == 0 && out.prof) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    unsigned long long* tl = out.prof + slot * 4;
+    tl[0] = tl_t0;
+    tl[1] = __builtin_amdgcn_s_memrealtime();
+    tl[2] = ((unsigned long long)hw << 32) | xcc;
+    tl[3] = (unsigned long long)sim;
+  }
+#endif
 
   // ------------------------------------------------------------------ results
   if (lane < my && !isfinite(j1)) st |= MPCT_ST_NONFINITE_;
@@ -634,10 +684,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 
 namespace mpct {
 
-long long lds_bytes_for(const DevScenario& sc, int N2, int Nu) {
+long long lds_bytes_for(const DevScenario& sc, int N2, int Nu, bool ext) {
   (void)N2;
   const int M = sc.nu * Nu;
-  LdsLayout L = lds_layout(sc, M);
+  LdsLayout L = lds_layout(sc, M, ext);
   return (long long)L.total * 8;
 }
 
@@ -649,12 +699,12 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
                     const DevOpts& o, const DevResult& out, const int* perm, int mlo, int first,
                     hipStream_t stream, std::string* err) {
   const int nu_cls = sc.numax < MAXM / sc.nu ? sc.numax : MAXM / sc.nu;  // largest Nu of this class
-  const long long lds = lds_bytes_for(sc, sc.n2max, nu_cls);
+  const bool ext = o.open_loop || o.want_traj;
+  const long long lds = lds_bytes_for(sc, sc.n2max, nu_cls, ext);
   if (lds > 160 * 1024) {
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
-  const bool ext = o.open_loop || o.want_traj;
   auto kern = sc.dtc ? (ext ? gpc_closed_loop_kernel<MAXM, true, true> : gpc_closed_loop_kernel<MAXM, true, false>)
                      : (ext ? gpc_closed_loop_kernel<MAXM, false, true> : gpc_closed_loop_kernel<MAXM, false, false>);
   if (lds > 64 * 1024) {

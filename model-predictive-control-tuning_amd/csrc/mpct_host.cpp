@@ -29,7 +29,7 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
                        const double* delta, const double* lambda, const double* r,
                        const double* v, const DevOpts& o, const DevResult& out, int maxM,
                        WorkOrder* wo, LaunchFan* fan, hipStream_t stream, std::string* err);
-long long lds_bytes_for(const DevScenario& sc, int N2, int Nu);
+long long lds_bytes_for(const DevScenario& sc, int N2, int Nu, bool ext);
 std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext);
 // defined in mdband_kernel.hip
 int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
@@ -947,6 +947,14 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
   (void)hipMalloc(&dprof, sizeof(unsigned long long) * S * PROF_N);
   dr.prof = dprof;
 #endif
+#ifdef MPCT_TIMELINE
+  // diagnostic build: [slot][t0, t1, HW_ID << 32 | XCC_ID, sim] -> $MPCT_TIMELINE_OUT
+  const long long S = C * nref;
+  unsigned long long* dprof = nullptr;
+  (void)hipMalloc(&dprof, sizeof(unsigned long long) * S * 4);
+  (void)hipMemset(dprof, 0, sizeof(unsigned long long) * S * 4);
+  dr.prof = dprof;
+#endif
   std::string err;
   int rc;
   if (s->nmpc)
@@ -957,6 +965,22 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
     rc = launch_closed_loop(cx->ds, C, nref, N2, Nu, delta, lambda, r, v, dop, dr, s->nu * s->numax, &cx->order, &cx->fan,
                             stream, &err);
   if (rc) return fail(rc, err);
+#ifdef MPCT_TIMELINE
+  {
+    std::vector<unsigned long long> hp(S * 4);
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpy(hp.data(), dprof, sizeof(unsigned long long) * S * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dprof);
+    const char* path = getenv("MPCT_TIMELINE_OUT");
+    if (path) {
+      FILE* f = fopen(path, "wb");
+      if (f) {
+        fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+        fclose(f);
+      }
+    }
+  }
+#endif
 #ifdef MPCT_PROFILE
   {
     std::vector<unsigned long long> hp(S * PROF_N);
@@ -1294,5 +1318,5 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.my = s->my;
   ds.nd = s->nd;
   compact_taps(s, ds);
-  return s->mdband ? mdband_lds_bytes(ds, N2, Nu, 2) : lds_bytes_for(ds, N2, Nu);
+  return s->mdband ? mdband_lds_bytes(ds, N2, Nu, 2) : lds_bytes_for(ds, N2, Nu, true);
 }

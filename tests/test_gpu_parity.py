@@ -185,10 +185,12 @@ def test_dispatch_key_mixed_horizons_and_step_refs(built):
         assert np.array_equal(st, rev.status.reshape(C, -1)[::-1])
         assert np.array_equal(res.J1, rev.J1.reshape(C, -1, 3)[::-1].reshape(res.J1.shape), equal_nan=True)
         # unit steps drive a few aggressive candidates into the QP iteration cap (status 1) on
-        # both sides; compare the simulations that are clean on both
+        # both sides; which ones is rounding-sensitive (degenerate active sets: the Givens and the
+        # Householder prologue QR agree to 3e-12 on every clean simulation here and differ by one
+        # capped simulation of 960, tools/diag/qr_status_ab.py); compare the ones clean on both
         cst = np.asarray(ref["status"]).reshape(C, -1)
         ok = np.all(st == 0, axis=1) & np.all(cst == 0, axis=1)
-        assert ok[3:].mean() > 0.97, ok[3:].mean()
+        assert ok[3:].mean() > 0.96, ok[3:].mean()
         a = res.J1.reshape(C, -1)[ok]
         b = np.asarray(ref["J1"]).reshape(C, -1)[ok]
         assert _rel(a, b) < COST_RTOL, _rel(a, b)
