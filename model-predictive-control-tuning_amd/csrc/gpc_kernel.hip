@@ -24,6 +24,7 @@
 #include "mpct_dev.h"
 #include "gi_core.h"
 #include "gpc_qp.h"
+#include "gpc_qp16.h"
 
 #ifndef MPCT_WAVES_PER_EU
 #define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
@@ -31,6 +32,9 @@
 #endif
 #ifndef MPCT_WAVES32
 #define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
+#endif
+#ifndef MPCT_EXP_OLDQP16
+#define MPCT_EXP_OLDQP16 0  // probes: the LDS-factor QP of gpc_qp.h in the M <= 16 class
 #endif
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
@@ -55,12 +59,13 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   LdsLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
+  const bool regqp = M <= 16;  // the M <= 16 class keeps J and d in VGPRs (gpc_qp16.h)
   L.rinv = take(M * M);
-  L.jt = take(M * M);        // J of the active-set method, column-major JT[k*M + i] = J(i,k)
-  L.dv = take(M);            // d = J'n_p
+  L.jt = take(regqp ? 0 : M * M);  // J of the active-set method, column-major JT[k*M + i] = J(i,k)
+  L.dv = take(regqp ? 0 : M);      // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
-  L.gb = take(MPCT_GI_B ? M * M : 0);  // B = R_A^-1 (row-major)
+  L.gb = take(regqp ? 16 * 16 : (MPCT_GI_B ? M * M : 0));  // B = R_A^-1 (row-major; stride 16 in the M <= 16 class)
   L.gw = take(MPCT_GI_B ? M : 0);      // warm start: w = R_A^-T c
   L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
   L.x = take(nx + 1);
@@ -69,7 +74,9 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   L.yprev = take(my);
   L.ucum = take(ext ? M : 0);
   L.ye = take(ncp * ne);
-  L.yeh = take(sc.regpath ? 0 : ncp * ne * kYeHist);  // register-resident histories need none
+  // plant entry output histories: the register path of the wide classes needs none; the M <= 16
+  // class keeps them here (its row-packed plant holds only one tap per lane)
+  L.yeh = take(sc.regpath && !regqp ? 0 : ncp * ne * kYeHist);
   L.uring = take(ncp * nin * kURing);
   L.mzh = take(nmz * kYeHist);   // DTC: model entry output histories
   L.smz = take(nmz);             // DTC: model entry outputs of the step
@@ -236,7 +243,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     const double di = fabs(dl[lane]);
     sqv = sc.wsq ? di : sqrt(di);
   }
-  double* sR = lds + L.jt;  // R (upper, row-major) parks in J's region until the QP starts
+  // R (upper, row-major) parks in J's region (R_A's in the M <= 16 class) until the QP starts
+  double* sR = lds + (MAXM <= 16 ? L.ra : L.jt);
   for (int pass = 0; pass < npass; ++pass) {
     const int vc = pass * vper + (lane - M);  // this lane's V column in this pass
     const bool vlane = lane >= M && vc < nx;
@@ -372,19 +380,25 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const int nyh_i = lane < my ? sc.nyhi[lane] : 0;
   const int upoff_n = lane < nu ? sc.upoff[lane] : 0;
   const int dum_n = lane < nu ? sc.dum[lane] : 0;
+  // QP row of the lane: in the M <= 16 class every 16-lane row block replicates the QP rows
+  const int qrow = MAXM <= 16 ? (lane & 15) : lane;
   RowCons rcn;
-  rcn.n = lane < M ? lane / Nu : 0;
-  rcn.l = lane < M ? lane - rcn.n * Nu : 0;
+  rcn.n = qrow < M ? qrow / Nu : 0;
+  rcn.l = qrow < M ? qrow - rcn.n * Nu : 0;
   rcn.dmin = sc.bnd[rcn.n];
   rcn.dmax = sc.bnd[nu + rcn.n];
   rcn.umin = sc.bnd[2 * nu + rcn.n];
   rcn.umax = sc.bnd[3 * nu + rcn.n];
-  const int ecopy = lane / ne;
-  const int ee = lane - ecopy * ne;
+  // plant entry of the lane; the M <= 16 class packs the entries row-wise: lane (e, k) = e + 16 k
+  // holds tap k of entry e (plant_packed below)
+  const bool plant_packed = MAXM <= 16 && sc.regpath != 0 && ((EXT && o.open_loop) ? 2 : 1) * ne <= 16;
+  const int elane = plant_packed ? (lane & 15) : lane;
+  const int ecopy = elane / ne;
+  const int ee = elane - ecopy * ne;
   const int ej = ee % nin;
-  const int e_nb = (lane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
-  const int e_na = (lane < ne * 2) ? sc.pl_na[pve + ee] : 0;
-  const int e_off = (lane < ne * 2) ? sc.pl_off[pve + ee] : 0;
+  const int e_nb = (elane < ne * 2) ? sc.pl_nb[pve + ee] : 0;
+  const int e_na = (elane < ne * 2) ? sc.pl_na[pve + ee] : 0;
+  const int e_off = (elane < ne * 2) ? sc.pl_off[pve + ee] : 0;
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 8 * M + 16;
   long long iters = 0;
@@ -393,6 +407,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 
   GIState<MAXM> gis;  // active-set factorisation carried across the steps (warm start)
   gi_reset<MAXM>(gis);
+  RegFactors rf;      // M <= 16 class: J in VGPRs, B = R_A^-1 in LDS (gpc_qp16.h), valid once gis.jinit
+  FOR4(r, rf.J[r] = 0.0;);
+  rf.sB = lds + L.gb;
   // unconstrained minimiser dU = A x, then the QP; result in sxc
   auto solve_step = [&]() __attribute__((always_inline)) {
     double xu = 0.0;
@@ -411,9 +428,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
           a1 += av.y * xa.y;
         }
       }
-      xu = row4_sum(a0 + a1);
+      xu = row4_sum(a0 + a1);  // row m of A . x on lanes m, m+16, m+32, m+48
       if (lane < M) sxc[lane] = xu;
-      if (lane >= M) xu = 0.0;
+      if (m >= M) xu = 0.0;
     } else if (lane < M) {
       // 16-byte LDS reads: two A entries of this row and two x entries per load
       const double2* arow = reinterpret_cast<const double2*>(sA + lane * nxp);
@@ -439,12 +456,17 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     lds_sync();
     PSTAMP(PROF_UNC);
 #ifndef MPCT_EXP_NOQP
-    const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
-    iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
+    if constexpr (MAXM <= 16 && !MPCT_EXP_OLDQP16) {
+      iters += gi_qp16(lds + L.rinv, lds + L.xc, lds + L.ra, lds + L.sl, M, Nu, rcn,
+                       qrow < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis, rf);
+    } else {
+      const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
+      iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
 #ifdef MPCT_PROFILE
-                         , pacc, pprev
+                           , pacc, pprev
 #endif
-    );
+      );
+    }
 #endif
     PSTAMP(PROF_QP);
   };
@@ -480,21 +502,33 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   // ------------------------------------------------------------------ closed loop
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
   const int ncopy = (EXT && o.open_loop) ? 2 : 1;
-  const bool is_entry = lane < ncopy * ne;
+  const bool is_entry = elane < ncopy * ne;
   const double* eb = splb + ee * sc.pl_maxb;
   const double* ea = spla + ee * sc.pl_maxa;
-  double* eyh = syeh + lane * kYeHist;
+  double* eyh = syeh + elane * kYeHist;
   const double* eur = sur + (ecopy * nin + ej) * kURing;
-  // register-resident per-lane state (regpath): plant entry taps / denominator / output history
-  double bt[kRegB], at[kRegA], yh[kRegA];
+  // register-resident per-lane state (regpath, wide classes): plant entry taps / denominator /
+  // output history
+  constexpr int kRB = MAXM <= 16 ? 1 : kRegB, kRA = MAXM <= 16 ? 1 : kRegA;
+  double bt[kRB], at[kRA], yh[kRA];
+  // M <= 16 class (plant_packed): lane (e, k) holds numerator tap k and denominator a_(k+1) of
+  // entry e; the output history stays in LDS, a step is one row4_sum over the four taps.  It holds
+  // 4 instead of 24 plant VGPRs, which the register QP (gpc_qp16.h) needs for three waves per SIMD
+  const int ktap = lane >> 4;
+  if constexpr (MAXM <= 16) {
+    bt[0] = (is_entry && ktap < e_nb - e_off) ? eb[e_off + ktap] : 0.0;
+    at[0] = (is_entry && ktap + 1 < e_na) ? ea[ktap + 1] : 0.0;
+    yh[0] = 0.0;
+  } else {
 #pragma unroll
-  for (int k = 0; k < kRegB; ++k) bt[k] = (is_entry && k < e_nb - e_off) ? eb[e_off + k] : 0.0;
+    for (int k = 0; k < kRegB; ++k) bt[k] = (is_entry && k < e_nb - e_off) ? eb[e_off + k] : 0.0;
 #pragma unroll
-  for (int k = 0; k < kRegA; ++k) {
-    at[k] = (is_entry && k + 1 < e_na) ? ea[k + 1] : 0.0;
-    yh[k] = 0.0;
+    for (int k = 0; k < kRegA; ++k) {
+      at[k] = (is_entry && k + 1 < e_na) ? ea[k + 1] : 0.0;
+      yh[k] = 0.0;
+    }
   }
-  const bool regpath = sc.regpath != 0;
+  const bool regpath = MAXM > 16 && sc.regpath != 0;
   // prefetched per-output signals
   double r_t = 0.0, yr_t = 0.0;
   if (lane < my) {
@@ -546,19 +580,28 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
+    if (!(MPCT_EXP_SKIP & 1) && plant_packed) {
+      // tap k of every entry on row block k (histories are zero before t = 0: no bound tests)
+      double pr = 0.0;
+      if (is_entry) pr = bt[0] * eur[(t - e_off - ktap) & (kURing - 1)] - at[0] * eyh[(t - 1 - ktap) & (kYeHist - 1)];
+      const double acc = row4_sum(pr);
+      if (lane < ncopy * ne) {
+        eyh[t & (kYeHist - 1)] = acc;
+        sye[lane] = acc;
+      }
+    } else if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double acc;
       if (regpath) {
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-        for (int k = 0; k < kRegB; ++k) a0 += bt[k] * eur[(t - e_off - k) & (kURing - 1)];
+        for (int k = 0; k < kRB; ++k) a0 += bt[k] * eur[(t - e_off - k) & (kURing - 1)];
 #pragma unroll
-        for (int k = 0; k < kRegA; ++k) a1 -= at[k] * yh[k];
+        for (int k = 0; k < kRA; ++k) a1 -= at[k] * yh[k];
         acc = a0 + a1;
 #pragma unroll
-        for (int k = kRegA - 1; k > 0; --k) yh[k] = yh[k - 1];
+        for (int k = kRA - 1; k > 0; --k) yh[k] = yh[k - 1];
         yh[0] = acc;
       } else {
         double a0 = 0.0, a1 = 0.0;
@@ -705,8 +748,12 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
+#ifdef MPCT_PROBE16  // register-allocation probes: compile the metric instance only (not a usable library)
+  auto kern = gpc_closed_loop_kernel<MAXM, false, false>;
+#else
   auto kern = sc.dtc ? (ext ? gpc_closed_loop_kernel<MAXM, true, true> : gpc_closed_loop_kernel<MAXM, true, false>)
                      : (ext ? gpc_closed_loop_kernel<MAXM, false, true> : gpc_closed_loop_kernel<MAXM, false, false>);
+#endif
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -774,8 +821,12 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const hipStream_t st = fs.stream(k);
     const int first = k == 0;
     if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
+#ifdef MPCT_PROBE16
+    else rc = -4;
+#else
     else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
+#endif
     mlo = cls;
     ++k;
   }

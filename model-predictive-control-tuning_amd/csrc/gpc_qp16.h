@@ -1,0 +1,483 @@
+// gpc_qp16.h — the per-step QP of the M <= 16 class of gpc_closed_loop_kernel with its factors in
+// VGPRs across all 64 lanes (no LDS round trip on the Goldfarb-Idnani iteration's chain).
+//
+// Same method as gpc_qp.h / gi_core.h (dual active set in J-form, warm-started across steps,
+// DESIGN.md §4-5), different data layout.  Lane l = i + 16 b (i = l & 15, b = l >> 4):
+//   * QP-row quantities ("row vectors": x, slacks, multipliers, constraint ids, active flags) are
+//     replicated: lane (i, b) holds entry i for every b, so the four 16-lane DPP rows compute the
+//     same thing and no broadcast is ever needed between them;
+//   * J (H^-1 = J J', 16 x 16) is held 4 entries per lane: lane (i, b) has J(i, 4b + r), r = 0..3
+//     ("RB"); B = R_A^-1 (explicit, upper triangular on the active block) is in LDS with row
+//     stride 16, so lane (i, b) reads its B(i, 4b..4b+3) with two 16-byte loads that do not depend
+//     on the iteration's d and issue under d's DPP reduction;
+//   * "column vectors" (d = J'n_p, w = B'c) come out of a 16-lane DPP reduction with entry 4b + r
+//     in register r of every lane of row b.
+// So y = X v (v a column vector) is 4 FMAs + one v_permlane16/32_swap reduction over b, and
+// y = X'v (v a row vector) is 4 multiplies + one DPP reduction within the 16-lane rows.  Per
+// iteration: d = J'n_p (DPP), then z = J(:,q:)d(q:), J(i,q), r = B d(0:q) and |d|^2, |d(q:)|^2 (one
+// permlane reduction each, independent), the ratio test, and the add (Householder on J's
+// registers, B's new column) or the drop.  R_A stays in LDS: only the drop's Givens chain reads it,
+// and B's column rotations ride on that chain's LDS round trips.  The triangular solves of gi_qp
+// (the warm start's R_A'w = c, lambda = R_A^-1 w, the dual direction r = R_A^-1 d) become products
+// with B (the MPCT_GI_B option of gi_core.h).  J and B in VGPRs both measured 190 VGPRs: the two
+// waves per SIMD that allows lost more at 4096 candidates than the shorter chain won.
+#pragma once
+#include "gi_core.h"
+
+namespace mpct {
+
+// four doubles of one lane.  Every element access uses a compile-time index (FOR4 expands its body
+// four times with a constexpr r), so SROA turns the arrays into registers before any other pass
+// runs: a #pragma unroll loop left a variable index for InstCombine to fold the uniform-index
+// selects into a dynamically indexed scratch load, and an ext_vector_type copied all 8 VGPRs of
+// the vector at every branch merge
+typedef double d4v[4];
+#define FOR4(r, ...)             \
+  do {                           \
+    { constexpr int r = 0; __VA_ARGS__ } \
+    { constexpr int r = 1; __VA_ARGS__ } \
+    { constexpr int r = 2; __VA_ARGS__ } \
+    { constexpr int r = 3; __VA_ARGS__ } \
+  } while (0)
+
+// J of one simulation (RB layout) and B = R_A^-1 in LDS (row-major, stride 16)
+struct RegFactors {
+  d4v J;
+  double* sB;
+};
+constexpr int kBS = 16;  // B's row stride
+
+// the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
+// hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
+// of it (three waves per SIMD = 168 VGPRs)
+__device__ __forceinline__ int qlane() {
+  int l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ int q16_i() { return qlane() & 15; }
+__device__ __forceinline__ int q16_b() { return qlane() >> 4; }
+
+// entry r (wave-uniform) of a lane's 4 registers.  The four values are passed by value: a
+// selection between loads through a reference would be folded (in the callee, before inlining)
+// into one load at a variable offset, which pins the caller's array to scratch
+__device__ __forceinline__ double sel4u_v(double x0, double x1, double x2, double x3, int r) {
+  double v = x0;
+  if (r == 1) v = x1;
+  if (r == 2) v = x2;
+  if (r == 3) v = x3;
+  return v;
+}
+#define sel4u(x, r) sel4u_v((x)[0], (x)[1], (x)[2], (x)[3], (r))
+// entry r (per lane, 0..3) of a lane's 4 registers
+__device__ __forceinline__ double sel4v_v(double x0, double x1, double x2, double x3, int r) {
+  const double lo = (r & 1) ? x1 : x0;
+  const double hi = (r & 1) ? x3 : x2;
+  return (r & 2) ? hi : lo;
+}
+#define sel4v(x, r) sel4v_v((x)[0], (x)[1], (x)[2], (x)[3], (r))
+
+// all-reduce of four values within every 16-lane row (four independent DPP chains)
+__device__ __forceinline__ void row16_sum4(d4v& t) {
+  FOR4(r, t[r] += dppd<kQx1>(t[r]););
+  FOR4(r, t[r] += dppd<kQx2>(t[r]););
+  FOR4(r, t[r] += dppd<kHalfMirror>(t[r]););
+  FOR4(r, t[r] += dppd<kMirror>(t[r]););
+}
+
+// column vector entry k (wave-uniform) as a scalar: register k & 3 of row k >> 2
+__device__ __forceinline__ double cvec_at(const d4v& c, int k) {
+  return bcast(sel4u(c, k & 3), (k >> 2) * 16);
+}
+
+// B(i, 4b..4b+3) of lane (i, b)
+__device__ __forceinline__ void b_row4(const double* sB, d4v& x) {
+  const double2* p = reinterpret_cast<const double2*>(sB + q16_i() * kBS + 4 * q16_b());
+  const double2 u = p[0], v = p[1];
+  x[0] = u.x;
+  x[1] = u.y;
+  x[2] = v.x;
+  x[3] = v.y;
+}
+
+// lane (i, b) receives lane (i, b + 1) / (i, b - 1): the rare Givens rotation across a register
+// block boundary (columns 4b + 3 and 4b + 4)
+__device__ __forceinline__ double rows_down(double v) { return __shfl(v, qlane() + 16, 64); }
+__device__ __forceinline__ double rows_up(double v) { return __shfl(v, qlane() - 16, 64); }
+
+// columns (jj, jj + 1) of J <- (c x_jj + s x_jj+1, -s x_jj + c x_jj+1).  jj is wave-uniform: a
+// scalar switch picks the register pair (a branch-free form with selects on every register took 9
+// more VGPRs)
+__device__ __forceinline__ void rot_pair(double& a, double& c, bool on, double cs, double sn) {
+  if (on) {
+    const double a0 = a, c0 = c;
+    a = cs * a0 + sn * c0;
+    c = -sn * a0 + cs * c0;
+  }
+}
+__device__ __forceinline__ void rb_rotate_cols(d4v& x, int jj, double cs, double sn) {
+  const int b = q16_b(), b0 = jj >> 2;
+  const bool on = b == b0;
+  switch (jj & 3) {
+    case 0: {
+      double a = x[0], c = x[1];
+      rot_pair(a, c, on, cs, sn);
+      x[0] = a;
+      x[1] = c;
+      break;
+    }
+    case 1: {
+      double a = x[1], c = x[2];
+      rot_pair(a, c, on, cs, sn);
+      x[1] = a;
+      x[2] = c;
+      break;
+    }
+    case 2: {
+      double a = x[2], c = x[3];
+      rot_pair(a, c, on, cs, sn);
+      x[2] = a;
+      x[3] = c;
+      break;
+    }
+    default: {  // columns 4 b0 + 3 and 4 (b0 + 1): across two register blocks
+      const double nx0 = rows_down(x[0]), pv3 = rows_up(x[3]);
+      if (on) x[3] = cs * x[3] + sn * nx0;
+      if (b == b0 + 1) x[0] = -sn * pv3 + cs * x[0];
+      break;
+    }
+  }
+}
+
+// box-constraint active flags on the replicated rows: bit kind of row m = p >> 2
+struct BoxMark16 {
+  template <class St>
+  __device__ __forceinline__ void operator()(St& S, int p, bool on) const {
+    if (q16_i() == (p >> 2)) {
+      if (on) S.act |= 1u << (p & 3);
+      else S.act &= ~(1u << (p & 3));
+    }
+  }
+};
+
+// J <- R^-1 (row-major in LDS, upper), B <- 0
+__device__ __forceinline__ void gi16_load_rinv(GIState<16>& S, RegFactors& F, const double* sRi, int M) {
+  const int i = q16_i(), b = q16_b();
+  FOR4(r, {
+    const int k = 4 * b + r;
+    F.J[r] = (i < M && k < M) ? sRi[i * M + k] : 0.0;
+  });
+  double2* p = reinterpret_cast<double2*>(F.sB + i * kBS + 4 * b);
+  p[0] = make_double2(0.0, 0.0);
+  p[1] = make_double2(0.0, 0.0);
+  S.nrot = 0;
+  S.jinit = true;
+}
+
+// d = J'n_p for constraint p (rows j0..mp of J, sign sg) -> column vector
+__device__ __forceinline__ void gi16_dvec(const RegFactors& F, int j0, int mp, double sg, d4v& d) {
+  const int i = q16_i();
+  const bool in = i >= j0 && i <= mp;
+  FOR4(r, d[r] = in ? F.J[r] : 0.0;);
+  row16_sum4(d);
+  FOR4(r, d[r] *= sg;);
+}
+
+// the products an iteration needs from d (column vector), q = active-set size, Bl = the lane's
+// B(i, 4b..4b+3):  z = J(:,q:)d(q:), jq = J(:,q), rk = B d(0:q) (row vectors), dn2 = |d|^2,
+// beta = |d(q:)|^2
+__device__ __forceinline__ void gi16_products(const RegFactors& F, const d4v& Bl, const d4v& d, int q,
+                                              double& z, double& jq, double& rk, double& dn2, double& beta) {
+  const int b = q16_b();
+  double za = 0.0, ra = 0.0, s1 = 0.0, s2 = 0.0;
+  FOR4(r, {
+    const bool tail = 4 * b + r >= q;
+    const double d2 = d[r] * d[r];
+    s1 += d2;
+    if (tail) {
+      za = fma(F.J[r], d[r], za);
+      s2 += d2;
+    } else {
+      ra = fma(Bl[r], d[r], ra);
+    }
+  });
+  const double jl = (b == (q >> 2)) ? sel4u(F.J, q & 3) : 0.0;
+  z = row4_sum(za);
+  jq = row4_sum(jl);
+  rk = row4_sum(ra);
+  dn2 = row4_sum(s1);
+  beta = row4_sum(s2);
+}
+
+// append constraint p: Householder on J(:,q:) mapping d(q:) to alpha e_q, B's column q and R_A's
+// column q (LDS), the multiplier upm and the id
+template <class Mark>
+__device__ __forceinline__ void gi16_add(GIState<16>& S, RegFactors& F, double* sRA, int M, int p,
+                                         const d4v& d, double beta, double z, double jq, double rk,
+                                         double upm, const Mark& mark) {
+  const int lane = qlane(), i = lane & 15, b = lane >> 4;
+  const int q = S.q;
+  const double dq = cvec_at(d, q);
+  const double nrm = MPCT_QP_FASTDIV ? beta * rsq_nr(beta) : sqrt(beta);  // beta > 0 on an add
+  const double alpha = dq > 0.0 ? -nrm : nrm;
+  const double vq = dq - alpha;
+  const double two_vtv = qp_rcp(beta - alpha * dq);  // 2 / v'v
+  const double f = (z - alpha * jq) * two_vtv;
+  const double ia = qp_rcp(alpha);
+  FOR4(r, {
+    const int k = 4 * b + r;
+    if (k >= q) F.J[r] = fma(-f, k == q ? vq : d[r], F.J[r]);
+  });
+  // B: column q = (-r / alpha; 1 / alpha), row q zero left of the diagonal (lanes = rows / columns)
+  if (lane <= q) F.sB[lane * kBS + q] = lane < q ? -rk * ia : ia;
+  if (lane < q) F.sB[q * kBS + lane] = 0.0;
+  // R_A(w, q) = d_w (w < q), R_A(q, q) = alpha: lanes (i < 4, b) write entry 4b + i
+  {
+    const int w = 4 * b + i;
+    if (i < 4 && w < q) sRA[w * M + q] = sel4v(d, i);
+    if (lane == 0) sRA[q * M + q] = alpha;
+  }
+  if (i == q) {
+    S.uw = upm;
+    S.ww = p;
+  }
+  mark(S, p, true);
+  S.q = q + 1;
+  S.nrot += 1;
+  lds_sync();  // B and R_A columns before the next read
+}
+
+// remove active constraint kd: R_A loses column kd and is re-triangularised by Givens rotations
+// (LDS, lanes = columns), applied to J's columns in registers and to B's columns in LDS (lanes =
+// rows); B then loses row kd
+template <class Mark>
+__device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double* sRA, int M, int kd,
+                                          const Mark& mark) {
+  const int lane = qlane(), i = lane & 15;
+  const int q = S.q;
+  double* sB = F.sB;
+  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
+  mark(S, idk, false);
+  lds_sync();  // R_A and B columns written by the adds
+  if (lane < q) {  // remove column kd (lanes = rows of row block 0)
+    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
+  }
+  {
+    const double un = lane_next<16>(S.uw);
+    const int wn = lane_next_i<16>(S.ww);
+    if (i >= kd && i < q - 1) {
+      S.uw = un;
+      S.ww = wn;
+    }
+  }
+  lds_sync();
+#pragma nounroll
+  for (int jj = kd; jj < q - 1; ++jj) {
+    const double a = sRA[jj * M + jj], c = sRA[(jj + 1) * M + jj];
+    const double rr = a * a + c * c;
+    if (rr != 0.0) {
+      const double ri = MPCT_QP_FASTDIV ? rsq_nr(rr) : 1.0 / sqrt(rr);
+      const double cs = a * ri, sn = c * ri;
+      if (lane >= jj && lane < q - 1) {
+        const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
+        sRA[jj * M + lane] = cs * r0 + sn * r1;
+        sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
+      }
+      if (lane < q) {  // B G': columns jj, jj + 1 (lanes = rows)
+        const double b0 = sB[lane * kBS + jj], b1 = sB[lane * kBS + jj + 1];
+        sB[lane * kBS + jj] = cs * b0 + sn * b1;
+        sB[lane * kBS + jj + 1] = -sn * b0 + cs * b1;
+      }
+      rb_rotate_cols(F.J, jj, cs, sn);
+      S.nrot += 1;
+    }
+    lds_sync();
+  }
+  // row kd of B G' leaves (lanes = columns)
+  if (lane < q - 1) {
+    for (int w = kd; w < q - 1; ++w) sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
+  }
+  const int qn = q - 1;
+  if (i == qn) {
+    S.uw = 0.0;
+    S.ww = -1;
+  }
+  S.q = qn;
+  lds_sync();
+}
+
+// the QP of one step (M <= 16): unconstrained minimiser xu (row vector), u(t-1) of the row's MV
+// up_row, the row's constraint data rc (both replicated over the four row blocks); result in sxc
+template <class Dummy = void>
+__device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* sRA, double* ssl, int M, int Nu,
+                                       const RowCons& rc, double up_row, double xu, double tol, int maxit,
+                                       int* st, GIState<16>& S, RegFactors& F) {
+  const int lane = qlane(), i = lane & 15;
+  const bool row = i < M;
+  if (!row) up_row = 0.0;
+  const int rl = rc.l;
+  const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
+  auto slacks = [&](double x, double s[4]) {
+    const double pre = block_prefix<16>(x, rl, Nu, row, sxc);
+    if (rl == 0) {
+      s[0] = x - lo_box;
+      s[1] = hi_box - x;
+      s[2] = INFINITY;
+      s[3] = INFINITY;
+    } else {
+      s[0] = x - rc.dmin;
+      s[1] = rc.dmax - x;
+      s[2] = pre - (rc.umin - up_row);
+      s[3] = (rc.umax - up_row) - pre;
+    }
+    if (!row) s[0] = s[1] = s[2] = s[3] = INFINITY;
+  };
+  const BoxMark16 mark{};
+  auto add = [&](int p, const d4v& d, double beta, double z, double jq, double rk, double upm)
+                 __attribute__((always_inline)) { gi16_add(S, F, sRA, M, p, d, beta, z, jq, rk, upm, mark); };
+  int it = 0;
+  double xm = xu;
+  {
+    double s[4];
+    slacks(xu, s);
+    const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
+    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
+    if (S.q == 0) {
+      S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
+    } else {
+      if (lane < M) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
+      }
+      if (!S.jinit || S.nrot >= MPCT_GI_REBUILD * M) {
+        // rebuild J and B for the retained set from R^-1, re-adding it in order
+        const int qq = S.q;
+        gi16_load_rinv(S, F, sRi, M);
+        S.q = 0;
+        for (int v = 0; v < qq; ++v) {
+          const int p = __builtin_amdgcn_readlane(S.ww, v);
+          int j0, mp;
+          double sg;
+          gi_normal(p, rc, j0, mp, sg);
+          d4v Bl, d;
+          lds_sync();
+          b_row4(F.sB, Bl);
+          gi16_dvec(F, j0, mp, sg, d);
+          double z, jq, rk, dn2, beta;
+          gi16_products(F, Bl, d, v, z, jq, rk, dn2, beta);
+          const double uk = S.uw;
+          add(p, d, beta, z, jq, rk, 0.0);
+          if (i == v) S.uw = uk;
+          ++it;
+        }
+        S.nrot = 0;
+      }
+      lds_sync();
+      // equality-constrained solve on the retained set, dropping negative multipliers:
+      // w = R_A^-T c = B'c, x = x_u + J(:,0:q) w, lambda = R_A^-1 w = B w
+      for (;;) {
+        const int q = S.q;
+        if (q == 0) {
+          xm = xu;
+          break;
+        }
+        const double c = i < q ? -ssl[S.ww] : 0.0;  // b_A - N_A'x_u
+        d4v Bl, w;
+        b_row4(F.sB, Bl);
+        FOR4(r, w[r] = i < q ? Bl[r] * c : 0.0;);
+        row16_sum4(w);
+        const int b = q16_b();
+        double xa = 0.0, la = 0.0;
+        FOR4(r, {
+          if (4 * b + r < q) {
+            xa = fma(F.J[r], w[r], xa);
+            la = fma(Bl[r], w[r], la);
+          }
+        });
+        xm = xu + row4_sum(xa);
+        const double lam = row4_sum(la);
+        if (i < q) S.uw = lam;
+        double lmin = i < q ? lam : INFINITY;
+        int kd = i;
+        qargmin<16>(lmin, kd, 0);
+        if (!(lmin < 0.0)) break;
+        gi16_drop(S, F, sRA, M, kd, mark);
+        ++it;
+      }
+      if (!row) xm = 0.0;
+    }
+  }
+  for (;;) {
+    // ---- most violated inactive constraint
+    double best = INFINITY;
+    int bid = 0x7fffffff;
+    {
+      double s[4];
+      slacks(xm, s);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (!((S.act >> k) & 1u) && s[k] < best) {
+          best = s[k];
+          bid = 4 * i + k;
+        }
+    }
+    qargmin<16>(best, bid, 2);
+    if (!(best < -tol)) break;
+    if (it >= maxit || S.q >= M) {
+      *st |= MPCT_ST_QP_MAXITER_;
+      break;
+    }
+    if (!S.jinit) gi16_load_rinv(S, F, sRi, M);
+    const int p = bid;
+    int j0, mp;
+    double sgp;
+    gi_normal(p, rc, j0, mp, sgp);
+    double sp = best;  // slack of p along the path
+    double upm = 0.0;  // its multiplier
+    bool infeas = false;
+    for (;;) {
+      ++it;
+      d4v Bl, d;
+      b_row4(F.sB, Bl);  // issues under d's reduction
+      gi16_dvec(F, j0, mp, sgp, d);
+      double zm, jq, rk, dn2, beta;
+      gi16_products(F, Bl, d, S.q, zm, jq, rk, dn2, beta);
+      // dual step over active constraints with r_w > 0
+      double t1 = INFINITY;
+      int kdrop = 0x7fffffff;
+      if (i < S.q && rk > 0.0) {
+        t1 = qp_div(S.uw, rk);
+        kdrop = i;
+      }
+      qargmin<16>(t1, kdrop, 0);
+      const double t2 = (beta > 1e-14 * dn2) ? -qp_div(sp, beta) : INFINITY;
+      const bool t2inf = __builtin_amdgcn_readfirstlane((int)(t2 == INFINITY)) != 0;
+      if (t1 == INFINITY && t2inf) {
+        *st |= MPCT_ST_QP_INFEAS_;
+        infeas = true;
+        break;
+      }
+      const bool full = __builtin_amdgcn_readfirstlane((int)(t2 <= t1)) != 0;
+      const double t = full ? t2 : t1;
+      if (!t2inf) xm += t * zm;
+      if (i < S.q) S.uw -= t * rk;
+      upm += t;
+      sp += t * beta;
+      if (full) {
+        add(p, d, beta, zm, jq, rk, upm);
+        break;
+      }
+      gi16_drop(S, F, sRA, M, kdrop, mark);
+      if (it >= maxit) {
+        *st |= MPCT_ST_QP_MAXITER_;
+        break;
+      }
+    }
+    if (it >= maxit || infeas) break;
+  }
+  if (lane < M) sxc[lane] = xm;
+  lds_sync();
+  return it;
+}
+
+}  // namespace mpct
