@@ -33,9 +33,6 @@
 #ifndef MPCT_WAVES32
 #define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
 #endif
-#ifndef MPCT_EXP_OLDQP16
-#define MPCT_EXP_OLDQP16 0  // probes: the LDS-factor QP of gpc_qp.h in the M <= 16 class
-#endif
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
 #endif
@@ -456,7 +453,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     lds_sync();
     PSTAMP(PROF_UNC);
 #ifndef MPCT_EXP_NOQP
-    if constexpr (MAXM <= 16 && !MPCT_EXP_OLDQP16) {
+    if constexpr (MAXM <= 16) {
       iters += gi_qp16(lds + L.rinv, lds + L.xc, lds + L.ra, lds + L.sl, M, Nu, rcn,
                        qrow < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis, rf);
     } else {
@@ -748,8 +745,12 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
-#ifdef MPCT_PROBE16  // register-allocation probes: compile the metric instance only (not a usable library)
-  auto kern = gpc_closed_loop_kernel<MAXM, false, false>;
+#ifdef MPCT_PROBE16  // register-allocation probes: compile one <16> instance only (not a usable library)
+#ifndef MPCT_PROBE_DTC
+#define MPCT_PROBE_DTC false
+#define MPCT_PROBE_EXT false
+#endif
+  auto kern = gpc_closed_loop_kernel<MAXM, MPCT_PROBE_DTC, MPCT_PROBE_EXT>;
 #else
   auto kern = sc.dtc ? (ext ? gpc_closed_loop_kernel<MAXM, true, true> : gpc_closed_loop_kernel<MAXM, true, false>)
                      : (ext ? gpc_closed_loop_kernel<MAXM, false, true> : gpc_closed_loop_kernel<MAXM, false, false>);
