@@ -244,7 +244,7 @@ __device__ __forceinline__ void gi16_add(GIState<16>& S, RegFactors& F, double* 
   mark(S, p, true);
   S.q = q + 1;
   S.nrot += 1;
-  lds_sync();  // B and R_A columns before the next read
+  lds_sync();  // B and R_A columns before the next read (ordering them only measured the same)
 }
 
 // remove active constraint kd: R_A loses column kd and is re-triangularised by Givens rotations

@@ -60,6 +60,22 @@ def main():
         # bench.py uses hbm_bytes_per_launch only when the library it loads has this hash
         "lib_sha256": open(os.path.join(src, "lib_sha256.txt")).read().split()[0],
     }
+    sqd = os.path.join(src, "sq")
+    if os.path.isdir(sqd):  # tools/gpu_evidence.sh: SQ instruction mix and LDS bank conflicts
+        import glob
+        agg = {}
+        for f in glob.glob(os.path.join(sqd, "*counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                if KERNEL in r["Kernel_Name"]:
+                    agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        med = {k: statistics.median(v) for k, v in agg.items()}
+        steps = a.candidates * 500.0
+        out["sq"] = {"per_launch_median": med,
+                     "per_sim_step": {k: med[k] / steps for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS",
+                                                                  "SQ_INSTS_VALU_FMA_F64", "SQ_WAVE_CYCLES") if k in med},
+                     "lds_bank_conflict_per_lds_active": med.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                     max(med.get("SQ_LDS_IDX_ACTIVE", 1.0), 1.0),
+                     "note": "SQ_WAVE_CYCLES in quad-cycles (MI355X_MICROARCH.md); tools/ab.py batch"}
     for name in (a.tag + "_pmc.json", "pmc_latest.json"):
         with open(os.path.join(dst, name), "w") as f:
             json.dump(out, f, indent=1)
