@@ -319,6 +319,10 @@ int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts* opts, char
  * error.  Lets a host check occupancy before launching. */
 int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu);
 
+/* The same for the instance a call with these options launches (opts NULL = costs only: the
+ * GAM_fun.m:81 call, which the tuning-grid benchmark times). */
+int64_t mpct_lds_bytes_opts(const mpct_scenario* s, const mpct_opts* opts, int32_t N2, int32_t Nu);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,9 @@
 #ifndef MPCT_WAVES32
 #define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
 #endif
+#ifndef MPCT_SIG_ASYNC
+#define MPCT_SIG_ASYNC 1  // step-loop signal prefetch waited for at the end of the step (r03p/q A/B)
+#endif
 #ifndef MPCT_EXP_SKIP
 #define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
 #endif
@@ -62,7 +65,7 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   L.dv = take(regqp ? 0 : M);      // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
-  L.gb = take(regqp ? 16 * 16 : (MPCT_GI_B ? M * M : 0));  // B = R_A^-1 (row-major; stride 16 in the M <= 16 class)
+  L.gb = take(regqp ? 16 * kBS : (MPCT_GI_B ? M * M : 0));  // B = R_A^-1 (row-major; stride kBS in the M <= 16 class)
   L.gw = take(MPCT_GI_B ? M : 0);      // warm start: w = R_A^-T c
   L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
   L.x = take(nx + 1);
@@ -455,7 +458,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #ifndef MPCT_EXP_NOQP
     if constexpr (MAXM <= 16) {
       iters += gi_qp16(lds + L.rinv, lds + L.xc, lds + L.ra, lds + L.sl, M, Nu, rcn,
-                       qrow < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis, rf);
+                       qrow < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis, rf
+#ifdef MPCT_PROFILE
+                       , pacc, pprev
+#endif
+      );
     } else {
       const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
       iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
@@ -553,6 +560,13 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       suprev[n] = un;
     }
   };
+#if MPCT_SIG_ASYNC
+  // the per-lane constants and r(0), Yref(0) loaded above are waited for here, once.  Left
+  // pending, their first use inside the step loop got an s_waitcnt vmcnt on every step (the
+  // compiler's wait is placed at the use, inside the loop), which also waited for that step's
+  // signal prefetch: its L2 latency was exposed every step
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
   for (int t = 0; t < nit; ++t) {
     // the lane predicates of the step are re-derived from an opaque copy of the lane id every
     // step: hoisted out of the loop they are kept as SGPR-pair exec masks, which the kernel's
@@ -560,10 +574,24 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     int ln = lane;
     asm volatile("" : "+v"(ln));
     double r_n = 0.0, yr_n = 0.0;
+#if MPCT_SIG_ASYNC
+    // prefetch r(t+1), Yref(t+1) with an explicit wait at the end of the step (compiled loads were
+    // waited for inside the same step, see the wait before the loop); every lane loads (clamped
+    // address), so no branch merges the loaded registers before the wait
+    {
+      const int si = lane < my ? lane : my - 1;
+      const int tn = t + 1 < nit ? t + 1 : t;
+      const double* pr = rr + si * nit + tn;
+      const double* py = sc.yref + si * nit + tn;
+      asm volatile("global_load_dwordx2 %0, %2, off\n\tglobal_load_dwordx2 %1, %3, off"
+                   : "=&v"(r_n), "=&v"(yr_n) : "v"(pr), "v"(py) : "memory");
+    }
+#else
     if (lane < my && t + 1 < nit) {  // prefetch t+1
       r_n = rr[lane * nit + t + 1];
       yr_n = sc.yref[lane * nit + t + 1];
     }
+#endif
     // inputs at time t that are already known: MDs v(t); open-loop uopt(t)
     if (sc.nd > 0) {
       for (int e = lane; e < ncopy * sc.nd; e += kWave) {
@@ -686,6 +714,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     if (!(MPCT_EXP_SKIP & 4)) solve_step();
     u_update(t, ln);
     lds_sync();
+#if MPCT_SIG_ASYNC
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(r_n), "+v"(yr_n) : : "memory");
+#endif
     r_t = r_n;
     yr_t = yr_n;
     PSTAMP(PROF_UUPD);

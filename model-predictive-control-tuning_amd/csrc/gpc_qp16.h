@@ -45,7 +45,14 @@ struct RegFactors {
   d4v J;
   double* sB;
 };
-constexpr int kBS = 16;  // B's row stride
+#ifndef MPCT_QP16_BS
+#define MPCT_QP16_BS 16
+#endif
+// B's row stride.  Stride 16 has the column writes of an add 16-way, the drop's column reads 8-way
+// and b_row4's row reads 4-way in LDS bank conflict (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+// 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
+// candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
+constexpr int kBS = MPCT_QP16_BS;
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
@@ -311,7 +318,11 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
 template <class Dummy = void>
 __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* sRA, double* ssl, int M, int Nu,
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
-                                       int* st, GIState<16>& S, RegFactors& F) {
+                                       int* st, GIState<16>& S, RegFactors& F
+#ifdef MPCT_PROFILE
+                                       , unsigned long long* pacc, unsigned long long& pprev
+#endif
+                                       ) {
   const int lane = qlane(), i = lane & 15;
   const bool row = i < M;
   if (!row) up_row = 0.0;
@@ -337,6 +348,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
                  __attribute__((always_inline)) { gi16_add(S, F, sRA, M, p, d, beta, z, jq, rk, upm, mark); };
   int it = 0;
   double xm = xu;
+  PSTAMP(PROF_QCHECK);
   {
     double s[4];
     slacks(xu, s);
@@ -407,6 +419,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
       if (!row) xm = 0.0;
     }
   }
+  PSTAMP(PROF_QWARM);
   for (;;) {
     // ---- most violated inactive constraint
     double best = INFINITY;
@@ -422,6 +435,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
         }
     }
     qargmin<16>(best, bid, 2);
+    PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
     if (it >= maxit || S.q >= M) {
       *st |= MPCT_ST_QP_MAXITER_;
@@ -442,6 +456,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
       gi16_dvec(F, j0, mp, sgp, d);
       double zm, jq, rk, dn2, beta;
       gi16_products(F, Bl, d, S.q, zm, jq, rk, dn2, beta);
+      PSTAMP(PROF_QD);
       // dual step over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
@@ -463,11 +478,14 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
       if (i < S.q) S.uw -= t * rk;
       upm += t;
       sp += t * beta;
+      PSTAMP(PROF_QR);
       if (full) {
         add(p, d, beta, zm, jq, rk, upm);
+        PSTAMP(PROF_QADD);
         break;
       }
       gi16_drop(S, F, sRA, M, kdrop, mark);
+      PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;
         break;

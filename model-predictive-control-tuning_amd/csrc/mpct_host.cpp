@@ -1297,7 +1297,7 @@ extern "C" int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts*
   return (int32_t)nm.size();
 }
 
-extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {
+static int64_t lds_bytes_ext(const mpct_scenario* s, int32_t N2, int32_t Nu, bool ext) {
   if (!s) return fail(MPCT_EINVAL, "null scenario");
   if (s->nmpc) return nmpc_lds_bytes(s->nu * Nu, N2);
   DevScenario ds{};
@@ -1318,5 +1318,13 @@ extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu
   ds.my = s->my;
   ds.nd = s->nd;
   compact_taps(s, ds);
-  return s->mdband ? mdband_lds_bytes(ds, N2, Nu, 2) : lds_bytes_for(ds, N2, Nu, true);
+  return s->mdband ? mdband_lds_bytes(ds, N2, Nu, ext ? 2 : 1) : lds_bytes_for(ds, N2, Nu, ext);
+}
+
+extern "C" int64_t mpct_lds_bytes(const mpct_scenario* s, int32_t N2, int32_t Nu) {
+  return lds_bytes_ext(s, N2, Nu, true);
+}
+
+extern "C" int64_t mpct_lds_bytes_opts(const mpct_scenario* s, const mpct_opts* opts, int32_t N2, int32_t Nu) {
+  return lds_bytes_ext(s, N2, Nu, opts && (opts->open_loop || opts->want_traj));
 }

@@ -83,7 +83,7 @@ class MpctResult(C.Structure):
 
 EXPORTS = [
     "mpct_abi_version", "mpct_last_error", "mpct_scenario_create", "mpct_scenario_destroy",
-    "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes",
+    "mpct_scenario_table", "mpct_eval_batch", "mpct_eval_batch_device", "mpct_lds_bytes", "mpct_lds_bytes_opts",
     "mpct_nmpc_scenario_create", "mpct_eval_batch_multi", "mpct_shard_candidates", "mpct_kernel_instance",
     "mpct_rank_device",
 ]
@@ -139,6 +139,8 @@ def load():
     lib.mpct_eval_batch_device.restype = C.c_int32
     lib.mpct_lds_bytes.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     lib.mpct_lds_bytes.restype = C.c_int64
+    lib.mpct_lds_bytes_opts.argtypes = [C.c_void_p, C.POINTER(MpctOpts), C.c_int32, C.c_int32]
+    lib.mpct_lds_bytes_opts.restype = C.c_int64
     lib.mpct_eval_batch_multi.argtypes = [C.c_void_p, C.c_int32, c_int32_p] + batch_args[1:]
     lib.mpct_eval_batch_multi.restype = C.c_int32
     lib.mpct_shard_candidates.argtypes = [C.c_int64, C.c_int32, C.c_int32, c_int64_p, C.c_int64]

@@ -185,7 +185,11 @@ class Scenario:
         k = ["my", "nu", "nd", "n2_max", "nu_max", "tlen", "nx", "nyh", "nup"]
         return dict(zip(k, self.table(2).astype(int).tolist()))
 
-    def lds_bytes(self, N2=None, Nu=None) -> int:
+    def lds_bytes(self, N2=None, Nu=None, costs_only=False) -> int:
+        """LDS per workgroup with the open-loop leg / trajectories (or, costs_only, of the
+        cost-only instance GAM_fun.m:81 calls launch)."""
+        if costs_only:
+            return int(self.lib.mpct_lds_bytes_opts(self._h, None, N2 or self.n2_max, Nu or self.nu_max))
         return int(self.lib.mpct_lds_bytes(self._h, N2 or self.n2_max, Nu or self.nu_max))
 
     def close(self):
