@@ -45,14 +45,11 @@ struct RegFactors {
   d4v J;
   double* sB;
 };
-#ifndef MPCT_QP16_BS
-#define MPCT_QP16_BS 16
-#endif
 // B's row stride.  Stride 16 has the column writes of an add 16-way, the drop's column reads 8-way
 // and b_row4's row reads 4-way in LDS bank conflict (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
 // candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
-constexpr int kBS = MPCT_QP16_BS;
+constexpr int kBS = 16;
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
