@@ -138,6 +138,7 @@ def test_errors_are_reported(built):
     assert lib.mpct_scenario_create(None, C.byref(h)) == -1
     assert lib.mpct_scenario_table(None, 0, None, 0) == -1
     assert lib.mpct_lds_bytes(None, 30, 5) < 0
+    assert lib.mpct_lds_bytes_opts(None, None, 30, 5) < 0
 
     P = shell3x3_plant()
     yref = np.zeros((3, 50))
