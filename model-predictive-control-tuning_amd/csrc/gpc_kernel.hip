@@ -579,8 +579,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     // waited for inside the same step, see the wait before the loop); every lane loads (clamped
     // address), so no branch merges the loaded registers before the wait
     {
-      const int si = lane < my ? lane : my - 1;
       const int tn = t + 1 < nit ? t + 1 : t;
+      const int si = lane < my ? lane : my - 1;
       const double* pr = rr + si * nit + tn;
       const double* py = sc.yref + si * nit + tn;
       asm volatile("global_load_dwordx2 %0, %2, off\n\tglobal_load_dwordx2 %1, %3, off"

@@ -13,9 +13,11 @@
 #endif
 
 #ifndef MPCT_GI_REBUILD
-#define MPCT_GI_REBUILD 32  // J (and R_A) rebuilt from R^-1 after this many x M rotations in the M <= 16
-                            // class (8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than
-                            // 8 M, same metric-grid parity, profiles/r02k_gib_rebuild_ab.txt)
+#define MPCT_GI_REBUILD 128  // J (and R_A) rebuilt from R^-1 after this many x M rotations in the M <= 16
+                             // class (8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than
+                             // 8 M, profiles/r02k_gib_rebuild_ab.txt; with the register QP 128 M is
+                             // 3-4 % faster than 32 M at 4096 candidates, same metric-grid parity,
+                             // profiles/r03v_rebuild128_vptr_ab.txt)
 #endif
 #ifndef MPCT_GI_REBUILD_WIDE
 #define MPCT_GI_REBUILD_WIDE 8  // the <32> / <64> classes (config 4's M > 16 draws, long horizons):
