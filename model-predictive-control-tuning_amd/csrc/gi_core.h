@@ -4,14 +4,13 @@
 #pragma once
 #include "wave_ops.h"
 
-#ifndef MPCT_QP_FASTDIV
-#define MPCT_QP_FASTDIV 1  // QP step lengths, Householder / Givens scalars by rcp_nr / rsq_nr (0: IEEE / and sqrt)
-#endif
-
 namespace mpct {
 
-__device__ __forceinline__ double qp_div(double a, double b) { return MPCT_QP_FASTDIV ? a * rcp_nr(b) : a / b; }
-__device__ __forceinline__ double qp_rcp(double b) { return MPCT_QP_FASTDIV ? rcp_nr(b) : 1.0 / b; }
+// QP step lengths and the Householder / Givens scalars are divide-free: v_rcp_f64 / v_rsq_f64 plus
+// two Newton steps (about 1 ulp; metric kernel 3.99 -> 3.87 ms, DESIGN.md §6 "Divide-free QP
+// scalars", profiles/r02i_qp_fastdiv_ab.txt)
+__device__ __forceinline__ double qp_div(double a, double b) { return a * rcp_nr(b); }
+__device__ __forceinline__ double qp_rcp(double b) { return rcp_nr(b); }
 
 // constraint p = 4*m + kind on move m = n*Nu + l:
 //   kind 0:  du_m >= lo     kind 1: -du_m >= -hi      (l == 0: merged rate/amplitude box)
@@ -51,8 +50,8 @@ struct RowCons {
 // lambda = R_A^-1 w), drops negative multipliers one at a time (x = EQP of the smaller set),
 // and then runs ordinary GI iterations from that dual-feasible point: the optimum of a strictly
 // convex QP is unique, so the result equals a cold start's up to rounding.  J is rebuilt from
-// R^-1 (re-adding the set) after MPCT_GI_REBUILD * M rotations (gpc_qp.h: 32 M in the M <= 16
-// class, 8 M above), which bounds the orthogonality drift of the rotated J.  Without a rebuild
+// R^-1 (re-adding the set) after kGiRebuild* x M rotations (gpc_qp.h: 128 M in the M <= 16
+// class, 32 M for its DTC instances, 8 M above), which bounds the orthogonality drift of the rotated J.  Without a rebuild
 // the metric grid drifted to 3.5e-5 relative; the 7.5e-10 bound was measured at the original
 // 4 M interval (C prototype).  At 32 M the metric grid's J1 still equals the C
 // port to 3.2e-9 (the same figure as at 4 M and 8 M); the wider classes keep 8 M.
@@ -135,52 +134,15 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
   return rk;
 }
 
-// Explicit B = R_A^-1 (row-major, stride M, leading q x q block valid), an optional companion of
-// R_A: the dual direction r = R_A^-1 d and the warm start's R_A'w = c, lambda = R_A^-1 w become
-// lane-parallel dot products instead of q-step serial substitutions (each step a v_readlane
-// broadcast and an LDS read).  An add appends column q (-r / alpha, 1 / alpha; row q zero left of
-// the diagonal), a drop rotates columns jj, jj+1 with the Givens rotations of R_A's rows and
-// removes row kd, since (G R_A E)^-1 = rows != kd of (R_A^-1 G').  Rebuilt with J.
-// r_w = sum_{c<q} B(w,c) v_c  (lane w < q; v in LDS, synchronised by the caller)
-__device__ __forceinline__ double gi_bdot(const double* sB, const double* sv, int q, int M) {
-  const int lane = qp_lane();
-  double a0 = 0.0, a1 = 0.0;
-  if (lane < q) {
-    const double* b = sB + lane * M;
-    int c = lane;  // upper triangular
-    for (; c + 1 < q; c += 2) {
-      a0 += b[c] * sv[c];
-      a1 += b[c + 1] * sv[c + 1];
-    }
-    if (c < q) a0 += b[c] * sv[c];
-  }
-  return a0 + a1;
-}
-// w_k = sum_{w<=k} B(w,k) v_w  (lane k < q): B'v
-__device__ __forceinline__ double gi_btdot(const double* sB, const double* sv, int q, int M) {
-  const int lane = qp_lane();
-  double a0 = 0.0, a1 = 0.0;
-  if (lane < q) {
-    int w = 0;
-    for (; w + 1 <= lane; w += 2) {
-      a0 += sB[w * M + lane] * sv[w];
-      a1 += sB[(w + 1) * M + lane] * sv[w + 1];
-    }
-    if (w <= lane) a0 += sB[w * M + lane] * sv[w];
-  }
-  return a0 + a1;
-}
-
-// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:));
-// with sB: rk = (R_A^-1 d(0:q))_lane on lanes < q
+// append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
 template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
-                                       const Mark& mark, double* sB = nullptr, double rk = 0.0) {
+                                       const Mark& mark) {
   const int lane = qp_lane();
   const int q = S.q;
   const double dq = bcast(dk, q);
-  const double nrm = MPCT_QP_FASTDIV ? beta * rsq_nr(beta) : sqrt(beta);  // beta > 0 on an add
+  const double nrm = beta * rsq_nr(beta);  // beta > 0 on an add
   const double alpha = dq > 0.0 ? -nrm : nrm;
   const double vq = dq - alpha;
   const double two_vtv = qp_rcp(beta - alpha * dq);  // 2 / v'v
@@ -198,13 +160,6 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     S.uw = upm;
     S.ww = p;
   }
-  if (sB) {
-    if (lane < q) {
-      sB[lane * M + q] = -rk * ia;
-      sB[q * M + lane] = 0.0;
-    }
-    if (lane == q) sB[q * M + q] = ia;
-  }
   mark(S, p, true);
   S.q = q + 1;
   S.nrot += 1;
@@ -214,7 +169,7 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
 template <int MAXM, class Mark>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
-                                        const Mark& mark, double* sB = nullptr) {
+                                        const Mark& mark) {
   const int lane = qp_lane();
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
@@ -237,7 +192,7 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
       const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
       const double rr = a * a + b * b;
       if (rr != 0.0) {
-        const double ri = MPCT_QP_FASTDIV ? rsq_nr(rr) : 1.0 / sqrt(rr);
+        const double ri = rsq_nr(rr);
         const double cs = a * ri, sn = b * ri;
         if (lane >= jj && lane < q - 1) {
           const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
@@ -249,18 +204,10 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
           sJT[jj * M + lane] = cs * j0v + sn * j1v;
           sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
         }
-        if (sB && lane < q) {  // B G': columns jj, jj+1 (lanes = rows)
-          const double b0 = sB[lane * M + jj], b1 = sB[lane * M + jj + 1];
-          sB[lane * M + jj] = cs * b0 + sn * b1;
-          sB[lane * M + jj + 1] = -sn * b0 + cs * b1;
-        }
         S.nrot += 1;
       }
       lds_sync();
     }
-  }
-  if (sB && lane < q - 1) {  // row kd of B G' leaves (lanes = columns)
-    for (int w = kd; w < q - 1; ++w) sB[w * M + lane] = sB[(w + 1) * M + lane];
   }
   const int qn = q - 1;
   if (lane == qn) {

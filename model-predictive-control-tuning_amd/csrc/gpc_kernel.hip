@@ -18,6 +18,8 @@
 //     M <= 16, the active-set QR runs lanes-as-rows entirely in registers;
 //   * a workgroup is exactly one wave: LDS hand-offs between lanes need only lgkmcnt(0) and a
 //     compiler fence (no s_barrier, no vmcnt drain of the prefetches).
+// Small plants in cost-only batches (the metric) run gpc_small_kernel (gpc_small.hip) instead; this
+// kernel is the general instance: any plant size, DTC mode, open-loop leg and trajectories.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -25,25 +27,17 @@
 #include "gi_core.h"
 #include "gpc_qp.h"
 #include "gpc_qp16.h"
-
-#ifndef MPCT_WAVES_PER_EU
-#define MPCT_WAVES_PER_EU 3  // M <= 16 class: 168 VGPRs = 3 waves per SIMD, which its LDS (13.4 KB at Shell 3x3) allows;
-                             // the larger classes are LDS-bound at 1-2 waves per CU and stay uncapped
-#endif
-#ifndef MPCT_WAVES32
-#define MPCT_WAVES32 1  // M <= 32 class: uncapped VGPRs (214 at DTC + cost only: two waves per SIMD)
-#endif
-#ifndef MPCT_SIG_ASYNC
-#define MPCT_SIG_ASYNC 1  // step-loop signal prefetch waited for at the end of the step (r03p/q A/B)
-#endif
-#ifndef MPCT_EXP_SKIP
-#define MPCT_EXP_SKIP 0  // ablation builds: bit 1 plant, 2 y update, 4 unconstrained solve, 8 u update
-#endif
+#include "gpc_prologue.h"
+#include "gpc_record.h"
 
 namespace mpct {
 
+// waves per SIMD the VGPR budget allows: 168 VGPRs = 3 in the M <= 16 class (its LDS, 13.4 KB at
+// Shell 3x3, allows that); the larger classes are LDS-bound at 1-2 workgroups per CU and uncapped
+constexpr int kWaves16 = 3;
+
 struct LdsLayout {
-  int rinv, jt, dv, ra, sl, gb, gw, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb,
+  int rinv, jt, dv, ra, sl, gb, A, x, xc, uprev, yprev, ucum, ye, yeh, uring, mzh, smz, frh, plb, pla, mzb,
       mza, frb, fra, total;
 };
 
@@ -65,8 +59,7 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   L.dv = take(regqp ? 0 : M);      // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
   L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
-  L.gb = take(regqp ? 16 * kBS : (MPCT_GI_B ? M * M : 0));  // B = R_A^-1 (row-major; stride kBS in the M <= 16 class)
-  L.gw = take(MPCT_GI_B ? M : 0);      // warm start: w = R_A^-T c
+  L.gb = take(regqp ? 16 * kBS : 0);  // M <= 16 class: B = R_A^-1 (row-major, stride kBS)
   L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
   L.x = take(nx + 1);
   L.xc = take(M);
@@ -87,36 +80,14 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   L.mza = take(nmz * (sc.dtc ? sc.mz_maxa : 0));
   L.frb = take(nfr * (sc.dtc ? sc.fr_max : 0));
   L.fra = take(nfr * (sc.dtc ? sc.fr_max : 0));
-#ifdef MPCT_EXP_LDS_PAD
-  take(MPCT_EXP_LDS_PAD);  // occupancy probes: doubles of padding
-#endif
   L.total = (o + 1) & ~1;
   return L;
-}
-
-// slacks of the 4 constraints of row m at x (x in LDS), up = u_prev of the row's MV
-__device__ __forceinline__ void row_slacks(const double* __restrict__ sxc, int m, const RowCons& rc,
-                                           double up, double s[4]) {
-  const double xm = sxc[m];
-  if (rc.l == 0) {
-    s[0] = xm - fmax(rc.dmin, rc.umin - up);
-    s[1] = fmin(rc.dmax, rc.umax - up) - xm;
-    s[2] = INFINITY;
-    s[3] = INFINITY;
-  } else {
-    double pre = 0.0;
-    for (int j = m - rc.l; j <= m; ++j) pre += sxc[j];
-    s[0] = xm - rc.dmin;
-    s[1] = rc.dmax - xm;
-    s[2] = pre - (rc.umin - up);
-    s[3] = (rc.umax - up) - pre;
-  }
 }
 
 // EXT: the open-loop prediction and/or trajectories may be requested; the EXT = false instance
 // (GAM scoring: costs only) carries none of their state through the step loop
 template <int MAXM, bool DTC, bool EXT>
-__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 32 ? MPCT_WAVES32 : 1))
+__global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
     gpc_closed_loop_kernel(const DevScenario sc, long long C, int nref,
                            const int* __restrict__ N2v, const int* __restrict__ Nuv,
                            const double* __restrict__ deltav, const double* __restrict__ lambdav,
@@ -147,35 +118,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 #endif
 
   // the cost record: caller's arrays at `sim`, or staging row xcd_row(slot) (ordered launches)
-  auto put_record = [&](double j1v, double j21v, double j22v, double jnuv, int status, long long itv)
-                        __attribute__((always_inline)) {
-    if (out.stage) {
-      const StageRow& R = out.srow;
-      double* row = out.stage + xcd_row(slot, C * nref) * R.w;
-      if (lane < my) {
-        if (R.j1 >= 0) row[R.j1 + lane] = j1v;
-        if (R.j21 >= 0) row[R.j21 + lane] = j21v;
-        if (R.j22 >= 0) row[R.j22 + lane] = j22v;
-      }
-      if (lane < nu && R.jnu >= 0) row[R.jnu + lane] = jnuv;
-      if (lane == 0) {
-        if (R.st >= 0) row[R.st] = (double)status;
-        if (R.it >= 0) row[R.it] = (double)itv;
-      }
-      return;
-    }
-    if (lane < my) {
-      if (out.J1) out.J1[sim * my + lane] = j1v;
-      if (out.j21) out.j21[sim * my + lane] = j21v;
-      if (out.j22) out.j22[sim * my + lane] = j22v;
-    }
-    if (lane < nu && out.Jnu) out.Jnu[sim * nu + lane] = jnuv;
-    if (lane == 0) {
-      if (out.status) out.status[sim] = status;
-      if (out.qp_iters) out.qp_iters[sim] = itv;
-    }
+  auto put = [&](double j1v, double j21v, double j22v, double jnuv, int status, long long itv)
+                 __attribute__((always_inline)) {
+    put_record(out, slot, C * nref, sim, sc.my, sc.nu, lane, j1v, j21v, j22v, jnuv, status, itv);
   };
-  auto write_nan = [&](int status) __attribute__((always_inline)) { put_record(NAN, NAN, NAN, NAN, status, 0); };
+  auto write_nan = [&](int status) __attribute__((always_inline)) { put(NAN, NAN, NAN, NAN, status, 0); };
   if (N2 <= 0) {
     if (first) write_nan(MPCT_ST_SKIPPED_);
     return;
@@ -220,159 +167,16 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   const double* lm = lambdav + c * nu;
   lds_sync();
 
-  // QR of W = [Q^1/2 G; Lambda^1/2] carrying V = [Q^1/2 Phi; 0], streaming W's rows in blocks of
-  // kHB (lane l < M owns column l of R, lane l >= M a column of T = Q1'V).  R's row k absorbs a
-  // block by one Householder reflection that annihilates the block's column k: x = [R_kk; w_.k],
-  // R_kk <- ||x|| (kept positive), v = x - ||x|| e1 with v_0 = -sigma / (R_kk + ||x||) (sigma =
-  // ||w_.k||^2: no cancellation), H = I - beta v v', beta = -1 / (||x|| v_0).  The reflection is
-  // decided by lane k and broadcast with v_readlane; per block of 8 rows it issues about half the
-  // VALU of 8 Givens rotations (one rsq / rcp chain per column instead of one per row).  When
-  // M + nx > 64 the V columns are processed in passes of 64 - M; every pass recomputes the same
-  // reflections (bitwise identical R), so T is exact.
-  constexpr int kHB = 8;
-  const int vper = kWave - M;  // V columns per pass (host guarantees M < 64)
-  const int npass = (nx + vper - 1) / vper;
-  double rcol[MAXM];
-  int gn = 0, gc = 0;
-  if (lane < M) {
-    gn = lane / Nu;
-    gc = lane - gn * Nu;
-  }
-  double sqv = 0.0;  // lane i < my: the output weight's square root (broadcast per row)
-  if (lane < my) {
-    const double di = fabs(dl[lane]);
-    sqv = sc.wsq ? di : sqrt(di);
-  }
-  // R (upper, row-major) parks in J's region (R_A's in the M <= 16 class) until the QP starts
+  // prologue (gpc_prologue.h): A = -R^-1 Q1'V row-major with padded rows, R^-1; R parks in
+  // J's region (R_A's in the M <= 16 class) until the QP starts
   double* sR = lds + (MAXM <= 16 ? L.ra : L.jt);
-  for (int pass = 0; pass < npass; ++pass) {
-    const int vc = pass * vper + (lane - M);  // this lane's V column in this pass
-    const bool vlane = lane >= M && vc < nx;
-    {
-      double wl0 = 0.0;
-      if (lane < M) {
-        const double ln = fabs(lm[lane / Nu]);
-        wl0 = sc.wsq ? ln : sqrt(ln);
-      }
-#pragma unroll
-      for (int k = 0; k < MAXM; ++k) rcol[k] = (k == lane) ? wl0 : 0.0;
-    }
-    // lane's entry of the next weighted row (output fi, prediction step fr) of
-    // [Q^1/2 G | Q^1/2 Phi]; zero rows past the end pad the last block
-    int fi = 0, fr = 0;
-    auto fetch = [&]() __attribute__((always_inline)) -> double {
-      double v = 0.0;
-      if (fi < my) {
-        if (lane < M) {
-          const int tt = sc.n1[fi] + fr - gc;
-          v = tt >= 0 ? sc.step[(fi * nu + gn) * sc.tlen + tt] : 0.0;  // prologue only: global (L2)
-        } else if (vlane) {
-          v = sc.phi[(long long)(fi * sc.n2max + fr) * nx + vc];
-        }
-        v *= bcast(sqv, fi);
-        if (++fr == N2) {
-          fr = 0;
-          ++fi;
-        }
-      }
-      return v;
-    };
-    auto reflect = [&](double (&w)[kHB], int k) __attribute__((always_inline)) {
-      double wk[kHB];
-      double sg0 = 0.0, sg1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < kHB; ++i) {
-        wk[i] = bcast(w[i], k);
-        if (i & 1) sg1 = fma(wk[i], wk[i], sg1);
-        else sg0 = fma(wk[i], wk[i], sg0);
-      }
-      const double sig = sg0 + sg1;
-      if (sig == 0.0) return;  // uniform: the block's column k is already zero
-      const double x0 = bcast(rcol[k], k);
-      const double rn = rsq_nr(fma(x0, x0, sig));  // 1 / ||x||
-      const double rs = rcp_nr(sig);
-      const double n = fma(x0, x0, sig) * rn;
-      const double xpn = x0 + n;
-      const double v0 = -sig * rcp_nr(xpn);
-      const double beta = rn * xpn * rs;  // -1 / (||x|| v_0)
-      double s0 = v0 * rcol[k], s1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < kHB; ++i) {
-        if (i & 1) s1 = fma(wk[i], w[i], s1);
-        else s0 = fma(wk[i], w[i], s0);
-      }
-      const double f = beta * (s0 + s1);
-      const bool own = lane == k;
-      rcol[k] = own ? n : fma(-f, v0, rcol[k]);
-#pragma unroll
-      for (int i = 0; i < kHB; ++i) w[i] = own ? 0.0 : fma(-f, wk[i], w[i]);
-    };
-    const int P = my * N2;
-    const int nblk = (P + kHB - 1) / kHB;
-    double nb[kHB];
-#pragma unroll
-    for (int i = 0; i < kHB; ++i) nb[i] = fetch();
-    for (int blk = 0; blk < nblk; ++blk) {
-      double w[kHB];
-#pragma unroll
-      for (int i = 0; i < kHB; ++i) w[i] = nb[i];
-      if (blk + 1 < nblk) {  // prefetch the next block (L2 latency under the reflections)
-#pragma unroll
-        for (int i = 0; i < kHB; ++i) nb[i] = fetch();
-      }
-#pragma unroll
-      for (int k = 0; k < MAXM; ++k)
-        if (k < M) reflect(w, k);
-    }
-    if (pass == 0) {  // R to LDS; singular R -> status
-      lds_sync();
-      if (lane < M) {
-#pragma unroll
-        for (int k = 0; k < MAXM; ++k)
-          if (k < M) sR[k * M + lane] = rcol[k];
-      }
-      lds_sync();
-      bool spd = true;
-      for (int k = 0; k < M; ++k)
-        if (!(sR[k * M + k] > 0.0)) spd = false;
-      if (!spd) {
-        write_nan(MPCT_ST_NONFINITE_);
-        return;
-      }
-    }
-    // A = -R^-1 T: V lanes solve for their own column, stored row-major A[m][vc]
-    if (vlane) {
-#pragma unroll
-      for (int kk = MAXM - 1; kk >= 0; --kk) {
-        if (kk < M) {
-          double a = rcol[kk];
-#pragma unroll
-          for (int j = 0; j < MAXM; ++j)
-            if (j > kk && j < M) a -= sR[kk * M + j] * rcol[j];
-          rcol[kk] = a / sR[kk * M + kk];
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < MAXM; ++m)
-        if (m < M) sA[m * nxp + vc] = -rcol[m];
-    }
+  if (!gpc_prologue<MAXM>(sc, lane, M, Nu, N2, dl, lm, sR, sRi, sA, nxp, nullptr)) {
+    write_nan(MPCT_ST_NONFINITE_);
+    return;
   }
   if (lane < M && nxp > nx) sA[lane * nxp + nx] = 0.0;  // pad column
-  // R^-1 (upper, row-major): lane j solves R x = e_j in its own LDS column (zeros below)
-  if (lane < M) {
-    for (int kk = lane; kk >= 0; --kk) {
-      double a = (kk == lane) ? 1.0 : 0.0;
-      for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[j * M + lane];
-      sRi[kk * M + lane] = a / sR[kk * M + kk];
-    }
-    for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
-  }
   lds_sync();
   PSTAMP(PROF_PROLOGUE);
-#ifdef MPCT_EXP_NOLOOP
-  if (lane == 0 && out.J1) out.J1[sim] = sA[lane] + sRi[lane];
-  return;
-#endif
 
   // per-lane constants of the step loop, defined after the prologue so that they are not live
   // (and spilled) across its register-heavy QR
@@ -429,7 +233,6 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         }
       }
       xu = row4_sum(a0 + a1);  // row m of A . x on lanes m, m+16, m+32, m+48
-      if (lane < M) sxc[lane] = xu;
       if (m >= M) xu = 0.0;
     } else if (lane < M) {
       // 16-byte LDS reads: two A entries of this row and two x entries per load
@@ -453,25 +256,26 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       xu = (a0 + a1) + (a2 + a3);
       sxc[lane] = xu;
     }
-    lds_sync();
+    if constexpr (MAXM > 16) lds_sync();
     PSTAMP(PROF_UNC);
-#ifndef MPCT_EXP_NOQP
     if constexpr (MAXM <= 16) {
-      iters += gi_qp16(lds + L.rinv, lds + L.xc, lds + L.ra, lds + L.sl, M, Nu, rcn,
-                       qrow < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis, rf
+      double xq;
+      iters += gi_qp16(lds + L.rinv, lds + L.ra, lds + L.sl, M, Nu, rcn, qrow < M ? suprev[rcn.n] : 0.0, xu,
+                       tol, maxit, &st, gis, rf, DTC ? kGiRebuild16Dtc : kGiRebuild16, xq
 #ifdef MPCT_PROFILE
                        , pacc, pprev
 #endif
       );
+      if (lane < M) sxc[lane] = xq;
+      lds_sync();
     } else {
-      const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl, lds + L.gb, lds + L.gw};
+      const QPBufs qb{lds + L.rinv, lds + L.xc, lds + L.jt, lds + L.dv, lds + L.ra, lds + L.sl};
       iters += gi_qp<MAXM>(qb, M, Nu, rcn, lane < M ? suprev[rcn.n] : 0.0, xu, tol, maxit, &st, gis
 #ifdef MPCT_PROFILE
                            , pacc, pprev
 #endif
       );
     }
-#endif
     PSTAMP(PROF_QP);
   };
 
@@ -541,7 +345,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   }
   // u(t) = u(t-1) + du(t, first move) of MV n = lane: past-control state, plant input ring
   auto u_update = [&](int t, int ln) __attribute__((always_inline)) {
-    if (!(MPCT_EXP_SKIP & 8) && ln < nu) {
+    if (ln < nu) {
       const int n = lane;
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
@@ -560,38 +364,17 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       suprev[n] = un;
     }
   };
-#if MPCT_SIG_ASYNC
   // the per-lane constants and r(0), Yref(0) loaded above are waited for here, once.  Left
   // pending, their first use inside the step loop got an s_waitcnt vmcnt on every step (the
   // compiler's wait is placed at the use, inside the loop), which also waited for that step's
   // signal prefetch: its L2 latency was exposed every step
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
   for (int t = 0; t < nit; ++t) {
     // the lane predicates of the step are re-derived from an opaque copy of the lane id every
     // step: hoisted out of the loop they are kept as SGPR-pair exec masks, which the kernel's
     // SGPR budget spills to VGPR lanes and reloads (v_readlane) several times per step
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    double r_n = 0.0, yr_n = 0.0;
-#if MPCT_SIG_ASYNC
-    // prefetch r(t+1), Yref(t+1) with an explicit wait at the end of the step (compiled loads were
-    // waited for inside the same step, see the wait before the loop); every lane loads (clamped
-    // address), so no branch merges the loaded registers before the wait
-    {
-      const int tn = t + 1 < nit ? t + 1 : t;
-      const int si = lane < my ? lane : my - 1;
-      const double* pr = rr + si * nit + tn;
-      const double* py = sc.yref + si * nit + tn;
-      asm volatile("global_load_dwordx2 %0, %2, off\n\tglobal_load_dwordx2 %1, %3, off"
-                   : "=&v"(r_n), "=&v"(yr_n) : "v"(pr), "v"(py) : "memory");
-    }
-#else
-    if (lane < my && t + 1 < nit) {  // prefetch t+1
-      r_n = rr[lane * nit + t + 1];
-      yr_n = sc.yref[lane * nit + t + 1];
-    }
-#endif
     // inputs at time t that are already known: MDs v(t); open-loop uopt(t)
     if (sc.nd > 0) {
       for (int e = lane; e < ncopy * sc.nd; e += kWave) {
@@ -605,7 +388,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
     }
     lds_sync();
     // plant entries y_e(t) (copy 0: closed loop, copy 1: open loop driven by uopt)
-    if (!(MPCT_EXP_SKIP & 1) && plant_packed) {
+    if (plant_packed) {
       // tap k of every entry on row block k (histories are zero before t = 0: no bound tests)
       double pr = 0.0;
       if (is_entry) pr = bt[0] * eur[(t - e_off - ktap) & (kURing - 1)] - at[0] * eyh[(t - 1 - ktap) & (kYeHist - 1)];
@@ -614,7 +397,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         eyh[t & (kYeHist - 1)] = acc;
         sye[lane] = acc;
       }
-    } else if (!(MPCT_EXP_SKIP & 1) && ln < ncopy * ne) {
+    } else if (ln < ncopy * ne) {
       // histories are zero before t = 0, so no t - l >= 0 test: loads issue back to back
       // only the nonzero taps (the delay's leading zeros are skipped: pl_off)
       double acc;
@@ -659,7 +442,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
       }
       lds_sync();
     }
-    if (!(MPCT_EXP_SKIP & 2) && ln < my) {
+    if (ln < my) {
       const int i = lane;
       double y = 0.0;
       for (int j = 0; j < nin; ++j) y += sye[i * nin + j];
@@ -709,14 +492,21 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
         if ((EXT && o.open_loop) && out.ys) out.ys[(sim * my + i) * nit + t] = ysv;
       }
     }
+    // prefetch r(t+1), Yref(t+1) (every lane loads, clamped address): issued after this step's
+    // last use of r(t), Yref(t), so the compiler's wait for them lands in the next step's y update,
+    // a whole step after the loads left
+    double r_n, yr_n;
+    {
+      const int tn = t + 1 < nit ? t + 1 : t;
+      const int si = lane < my ? lane : my - 1;
+      r_n = rr[si * nit + tn];
+      yr_n = sc.yref[si * nit + tn];
+    }
     lds_sync();
     PSTAMP(PROF_YUPD);
-    if (!(MPCT_EXP_SKIP & 4)) solve_step();
+    solve_step();
     u_update(t, ln);
     lds_sync();
-#if MPCT_SIG_ASYNC
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(r_n), "+v"(yr_n) : : "memory");
-#endif
     r_t = r_n;
     yr_t = yr_n;
     PSTAMP(PROF_UUPD);
@@ -740,8 +530,8 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
   // ------------------------------------------------------------------ results
   if (lane < my && !isfinite(j1)) st |= MPCT_ST_NONFINITE_;
   const unsigned long long nf = __ballot(st & MPCT_ST_NONFINITE_);
-  put_record(j1, (EXT && o.open_loop) ? j21 : NAN, j22, (EXT && o.open_loop) ? jnu : NAN,
-             st | (nf ? MPCT_ST_NONFINITE_ : 0), iters);
+  put(j1, (EXT && o.open_loop) ? j21 : NAN, j22, (EXT && o.open_loop) ? jnu : NAN,
+      st | (nf ? MPCT_ST_NONFINITE_ : 0), iters);
 }
 
 }  // namespace mpct
@@ -755,9 +545,15 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_WAVES_PER_EU : (MAXM <= 
 
 namespace mpct {
 
+long long small_lds_bytes(int M);  // gpc_small.hip
+int launch_small(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
+                 const double* lambda, const double* r, const DevOpts& o, const DevResult& out, const int* perm,
+                 int first, hipStream_t stream, std::string* err);
+
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu, bool ext) {
   (void)N2;
   const int M = sc.nu * Nu;
+  if (sc.small && !ext && M <= 16) return small_lds_bytes(M);
   LdsLayout L = lds_layout(sc, M, ext);
   return (long long)L.total * 8;
 }
@@ -776,16 +572,8 @@ static int launch_t(const DevScenario& sc, long long C, int nref, const int* N2,
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;
   }
-#ifdef MPCT_PROBE16  // register-allocation probes: compile one <16> instance only (not a usable library)
-#ifndef MPCT_PROBE_DTC
-#define MPCT_PROBE_DTC false
-#define MPCT_PROBE_EXT false
-#endif
-  auto kern = gpc_closed_loop_kernel<MAXM, MPCT_PROBE_DTC, MPCT_PROBE_EXT>;
-#else
   auto kern = sc.dtc ? (ext ? gpc_closed_loop_kernel<MAXM, true, true> : gpc_closed_loop_kernel<MAXM, true, false>)
                      : (ext ? gpc_closed_loop_kernel<MAXM, false, true> : gpc_closed_loop_kernel<MAXM, false, false>);
-#endif
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -815,7 +603,13 @@ std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext) {
   std::string nm;
   for (int cls = 16; cls <= top_class(maxM); cls *= 2) {
     if (sc.nu > cls) continue;
-    nm += (nm.empty() ? "gpc_closed_loop_kernel<" : " + <") + std::to_string(cls) + tail;
+    if (cls == 16 && sc.small && !ext) {
+      nm = "gpc_small_kernel";
+      continue;
+    }
+    if (nm.empty()) nm = "gpc_closed_loop_kernel<" + std::to_string(cls) + tail;
+    else if (nm == "gpc_small_kernel") nm += " + gpc_closed_loop_kernel<" + std::to_string(cls) + tail;
+    else nm += " + <" + std::to_string(cls) + tail;
   }
   return nm;
 }
@@ -852,13 +646,11 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     }
     const hipStream_t st = fs.stream(k);
     const int first = k == 0;
-    if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
-#ifdef MPCT_PROBE16
-    else rc = -4;
-#else
+    const bool ext = o.open_loop || o.want_traj;
+    if (cls == 16 && sc.small && !ext) rc = launch_small(sc, C, nref, N2, Nu, delta, lambda, r, o, lo, perm, first, st, err);
+    else if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
-#endif
     mlo = cls;
     ++k;
   }

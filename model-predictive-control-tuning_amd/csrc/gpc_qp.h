@@ -5,25 +5,15 @@
 #pragma once
 #include "gi_core.h"
 
-#ifndef MPCT_GI_B
-// explicit R_A^-1 (gi_core.h gi_bdot): parallel dot products instead of serial solves.  Off: on the
-// metric grid it saves 1.6-3 % at one workgroup per CU but its M^2 of LDS per simulation costs
-// two workgroups per CU, 14 % at 8192 candidates (profiles/r02f_quad_experiment.txt)
-#define MPCT_GI_B 0
-#endif
-
-#ifndef MPCT_GI_REBUILD
-#define MPCT_GI_REBUILD 128  // J (and R_A) rebuilt from R^-1 after this many x M rotations in the M <= 16
-                             // class (8 M: 5 % faster than 4 M; 32 M: 1.5 % faster than
-                             // 8 M, profiles/r02k_gib_rebuild_ab.txt; with the register QP 128 M is
-                             // 3-4 % faster than 32 M at 4096 candidates, same metric-grid parity,
-                             // profiles/r03v_rebuild128_vptr_ab.txt)
-#endif
-#ifndef MPCT_GI_REBUILD_WIDE
-#define MPCT_GI_REBUILD_WIDE 8  // the <32> / <64> classes (config 4's M > 16 draws, long horizons):
-                                // longer active sets apply more rotations per add, and 32 M was only
-                                // measured on the metric class, so they keep the 8 M interval
-#endif
+// J (and R_A) are rebuilt from R^-1 after this many x M rotations.  M <= 16 class:
+// 8 M was 5 % faster than 4 M, 32 M 1.5 % faster than 8 M (profiles/r02k_gib_rebuild_ab.txt), and
+// with the register QP 128 M 3-4 % faster than 32 M at 4096 candidates with the same metric-grid
+// parity (profiles/r03v_rebuild128_vptr_ab.txt).  DTC instances (config 4's mismatch draws) keep
+// 32 M: 128 M was never measured where the interval actually fires on them.  The <32> / <64>
+// classes keep 8 M (longer active sets apply more rotations per add).
+constexpr int kGiRebuild16 = 128;
+constexpr int kGiRebuild16Dtc = 32;
+constexpr int kGiRebuildWide = 8;
 
 namespace mpct {
 
@@ -40,7 +30,6 @@ struct QPBufs {
   const double* rinv;  // R^-1 (row-major)
   double *xc;          // in: -, out: the optimal moves (lanes < M)
   double *jt, *dv, *ra, *sl;
-  double *b, *w;       // B = R_A^-1 and the warm start's w (MPCT_GI_B)
 };
 
 // the QP of one step: unconstrained minimiser xu (lanes < M), u(t-1) of the lane's MV up_row
@@ -59,8 +48,6 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
   double* sd = Q.dv;
   double* sRA = Q.ra;
   double* ssl = Q.sl;
-  double* sB = MPCT_GI_B ? Q.b : nullptr;
-  double* sw = Q.w;
   if (!row) up_row = 0.0;
   const int rl = rc.l;  // the lane's position in its MV block
   const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
@@ -94,7 +81,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
 #pragma unroll
         for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
       }
-      if (!S.jinit || S.nrot >= (MAXM <= 16 ? MPCT_GI_REBUILD : MPCT_GI_REBUILD_WIDE) * M) {
+      if (!S.jinit || S.nrot >= kGiRebuildWide * M) {
         // rebuild J (and R_A) for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
         gi_load_rinv<MAXM>(S, sJT, sRi, M, row);
@@ -108,9 +95,8 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
           const double beta = qsum<MAXM>(lane >= v ? dk * dk : 0.0);
           lds_sync();
           const double zm = gi_z(sJT, sd, v, M, row);
-          const double rv = MPCT_GI_B ? gi_bdot(sB, sd, v, M) : 0.0;
           const double uk = S.uw;
-          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row, BoxMark{}, sB, rv);
+          gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, 0.0, row, BoxMark{});
           if (lane == v) S.uw = uk;
           ++it;
         }
@@ -128,24 +114,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
         if (lane < q) c = -ssl[S.ww];  // b_A - N_A'x_u
         double lam;
         xm = xu;
-        if constexpr (MPCT_GI_B) {  // w = B'c, x = x_u + J(:,0:q) w, lambda = B w
-          if (lane < q) sd[lane] = c;
-          lds_sync();
-          const double wk = gi_btdot(sB, sd, q, M);
-          if (lane < q) sw[lane] = wk;
-          lds_sync();
-          if (row) {
-            double x1 = 0.0;
-            int v = 0;
-            for (; v + 1 < q; v += 2) {
-              xm += sJT[v * M + lane] * sw[v];
-              x1 += sJT[(v + 1) * M + lane] * sw[v + 1];
-            }
-            if (v < q) xm += sJT[v * M + lane] * sw[v];
-            xm += x1;
-          }
-          lam = gi_bdot(sB, sw, q, M);
-        } else {
+        {
           double wv = 0.0;
           for (int v = 0; v < q; ++v) {  // forward substitution R_A'w = c, x = x_u + J(:,0:q) w
             const double w = bcast(c * S.rdg, v);
@@ -160,16 +129,13 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{}, sB);
+        gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{});
         ++it;
       }
       if (!row) xm = 0.0;
     }
   }
   PSTAMP(PROF_QWARM);
-#ifdef MPCT_DEBUG_SIM
-  if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0) printf("QP entry-after-warm q=%d it=%d nrot=%d\n", S.q, it, S.nrot);
-#endif
   for (;;) {
     // ---- most violated inactive constraint
     double best = INFINITY;
@@ -208,7 +174,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
       lds_sync();
       const double zm = gi_z(sJT, sd, S.q, M, row);
       PSTAMP(PROF_QD);
-      const double rk = MPCT_GI_B ? gi_bdot(sB, sd, S.q, M) : gi_backsub<MAXM>(S, sRA, M, dk);
+      const double rk = gi_backsub<MAXM>(S, sRA, M, dk);
       // dual step over active constraints with r_w > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
@@ -226,20 +192,16 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
       }
       const bool full = t2 <= t1;
       const double t = full ? t2 : t1;
-#ifdef MPCT_DEBUG_SIM
-      if (blockIdx.x == MPCT_DEBUG_SIM && lane == 0 && it > 40 && it < 70)
-        printf("it=%d q=%d p=%d sp=%.3e beta=%.3e dn2=%.3e t1=%.3e t2=%.3e kd=%d %s\n", it, S.q, p, sp, beta, dn2, t1, t2, kdrop, full ? "ADD" : "DROP");
-#endif
       if (t2 != INFINITY) xm += t * zm;
       if (lane < S.q) S.uw -= t * rk;
       upm += t;
       sp += t * beta;
       if (full) {
-        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{}, sB, rk);
+        gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
         PSTAMP(PROF_QADD);
         break;
       }
-      gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{}, sB);
+      gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{});
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;

@@ -19,7 +19,7 @@
 // registers, B's new column) or the drop.  R_A stays in LDS: only the drop's Givens chain reads it,
 // and B's column rotations ride on that chain's LDS round trips.  The triangular solves of gi_qp
 // (the warm start's R_A'w = c, lambda = R_A^-1 w, the dual direction r = R_A^-1 d) become products
-// with B (the MPCT_GI_B option of gi_core.h).  J and B in VGPRs both measured 190 VGPRs: the two
+// with B.  J and B in VGPRs both measured 190 VGPRs: the two
 // waves per SIMD that allows lost more at 4096 candidates than the shorter chain won.
 #pragma once
 #include "gi_core.h"
@@ -222,7 +222,7 @@ __device__ __forceinline__ void gi16_add(GIState<16>& S, RegFactors& F, double* 
   const int lane = qlane(), i = lane & 15, b = lane >> 4;
   const int q = S.q;
   const double dq = cvec_at(d, q);
-  const double nrm = MPCT_QP_FASTDIV ? beta * rsq_nr(beta) : sqrt(beta);  // beta > 0 on an add
+  const double nrm = beta * rsq_nr(beta);  // beta > 0 on an add
   const double alpha = dq > 0.0 ? -nrm : nrm;
   const double vq = dq - alpha;
   const double two_vtv = qp_rcp(beta - alpha * dq);  // 2 / v'v
@@ -280,7 +280,7 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
     const double a = sRA[jj * M + jj], c = sRA[(jj + 1) * M + jj];
     const double rr = a * a + c * c;
     if (rr != 0.0) {
-      const double ri = MPCT_QP_FASTDIV ? rsq_nr(rr) : 1.0 / sqrt(rr);
+      const double ri = rsq_nr(rr);
       const double cs = a * ri, sn = c * ri;
       if (lane >= jj && lane < q - 1) {
         const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
@@ -311,11 +311,13 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
 }
 
 // the QP of one step (M <= 16): unconstrained minimiser xu (row vector), u(t-1) of the row's MV
-// up_row, the row's constraint data rc (both replicated over the four row blocks); result in sxc
+// up_row, the row's constraint data rc (both replicated over the four row blocks); the optimal
+// moves come back in xout (row vector, registers; xu itself when it is feasible).  rebuild: the
+// J rebuild interval in units of M rotations (gpc_qp.h)
 template <class Dummy = void>
-__device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* sRA, double* ssl, int M, int Nu,
+__device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, double* ssl, int M, int Nu,
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
-                                       int* st, GIState<16>& S, RegFactors& F
+                                       int* st, GIState<16>& S, RegFactors& F, int rebuild, double& xout
 #ifdef MPCT_PROFILE
                                        , unsigned long long* pacc, unsigned long long& pprev
 #endif
@@ -326,7 +328,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
   const int rl = rc.l;
   const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
   auto slacks = [&](double x, double s[4]) {
-    const double pre = block_prefix<16>(x, rl, Nu, row, sxc);
+    const double pre = block_prefix<16>(x, rl, Nu, row, nullptr);
     if (rl == 0) {
       s[0] = x - lo_box;
       s[1] = hi_box - x;
@@ -350,7 +352,10 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
     double s[4];
     slacks(xu, s);
     const double smin = fmin(fmin(s[0], s[1]), fmin(s[2], s[3]));
-    if (__ballot(smin < -tol) == 0) return 0;  // sxc already holds x_u (solve_step)
+    if (__ballot(smin < -tol) == 0) {  // x_u is feasible: optimal (the retained set is kept)
+      xout = xu;
+      return 0;
+    }
     if (S.q == 0) {
       S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
     } else {
@@ -358,7 +363,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
 #pragma unroll
         for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
       }
-      if (!S.jinit || S.nrot >= MPCT_GI_REBUILD * M) {
+      if (!S.jinit || S.nrot >= rebuild * M) {
         // rebuild J and B for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
         gi16_load_rinv(S, F, sRi, M);
@@ -490,8 +495,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sxc, double* s
     }
     if (it >= maxit || infeas) break;
   }
-  if (lane < M) sxc[lane] = xm;
-  lds_sync();
+  xout = xm;
   return it;
 }
 

@@ -32,6 +32,14 @@ constexpr int kRegA = 4;       // denominator coefficients a_1.. per plant entry
 constexpr int kRegDu = 8;      // past-control register length per MV (regpath eligibility)
 constexpr int kRegY = 6;       // y history (difference basis) length per output (regpath eligibility)
 constexpr int kWave = 64;
+// gpc_small_kernel (gpc_small.hip) layout constants, shared with the host tables it reads
+constexpr int kSmY = 12;                   // y difference state: columns of A's quarter 0
+constexpr int kSmR = 8;                    // past-control ring per MV: columns of quarters 1..3
+constexpr int kSmA = kSmY + 3 * kSmR;      // A row stride
+constexpr int kSmU = 16;                   // plant input ring per MV (power of two, > longest delay + taps)
+constexpr int kSmE = 4;                    // plant entry output ring (power of two, > denominator taps)
+constexpr int kSmEOff = 3 * kSmU;          // entry output rings after the input rings
+constexpr int kSmHist = kSmEOff + 16 * kSmE;
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
 constexpr int MPCT_ST_QP_MAXITER_ = 1;
@@ -56,6 +64,15 @@ struct DevScenario {
   int ne;                   // plant entries my*nin (nin = plant input columns incl. disturbances)
   int pl_maxb, pl_maxa;     // longest plant numerator (incl. delay) / denominator
   int regpath;              // every per-lane history / coefficient set fits the kReg* caps
+  // small plants (gpc_small_kernel eligibility, mpct_host.cpp small_plant) and its lane tables:
+  // plant term of lane L = 16 k + 4 i + j (coefficient, history ring offset in the kernel's history
+  // region, delay, ring mask) and the state column -> A column map
+  int small;
+  const double* sm_coef;  // [64]
+  const int* sm_hoff;     // [64]
+  const int* sm_hc;       // [64]
+  const int* sm_hmask;    // [64]
+  const int* sm_acol;     // [nx]
   // tables (device pointers into one allocation)
   const double* step;   // [my][nu][tlen]   model step responses s_ij(t), t = 0..tlen-1
   const double* phi;    // [my*n2max][nx]   free response rows (Diophantine F | deltaUFree Hp)

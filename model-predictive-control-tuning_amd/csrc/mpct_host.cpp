@@ -756,6 +756,55 @@ static int regpath(const mpct_scenario* s) {
   return rp ? 1 : 0;
 }
 
+// gpc_small_kernel's lane tables (gpc_small.hip), or false when the scenario is not a small plant:
+// my <= 4 outputs, nu <= 3 MVs, no MD / plant-only inputs, one plant, GPC mode, y difference state
+// <= kSmY entries (<= 4 per output), past-control registers <= kSmR, <= 4 plant terms per entry
+struct SmallTables {
+  std::vector<double> coef;
+  std::vector<int> hoff, hc, hmask, acol;
+};
+static bool small_plant(const mpct_scenario* s, SmallTables* tb = nullptr) {
+  if (s->mdband || s->nmpc || s->dtc || s->nd || s->nq || s->nvar != 1) return false;
+  if (s->my > 4 || s->nu > 3 || s->npin != s->nu || s->nyh > kSmY) return false;
+  for (int i = 0; i < s->my; ++i)
+    if (s->nyhi[i] > 4) return false;
+  for (int n = 0; n < s->nu; ++n)
+    if (s->dum[n] > kSmR) return false;
+  for (int e = 0; e < s->ne; ++e) {
+    const int nbz = s->pl_nb[e] - s->pl_off[e], na1 = s->pl_na[e] - 1;
+    if (nbz + na1 > 4 || na1 >= kSmE || s->pl_nb[e] > kSmU) return false;
+  }
+  if (!tb) return true;
+  tb->coef.assign(kWave, 0.0);
+  tb->hoff.assign(kWave, 0);
+  tb->hc.assign(kWave, 0);
+  tb->hmask.assign(kWave, kSmU - 1);
+  for (int L = 0; L < kWave; ++L) {
+    const int k = L >> 4, ep = L & 15, i = ep >> 2, j = ep & 3;
+    if (i >= s->my || j >= s->nu) continue;
+    const int e = i * s->npin + j;
+    const int off = s->pl_off[e], nbz = s->pl_nb[e] - off, na1 = s->pl_na[e] - 1;
+    if (k < nbz) {  // b tap: u_j(t - off - k)
+      tb->coef[L] = s->pl_b[(size_t)e * s->pl_maxb + off + k];
+      tb->hoff[L] = j * kSmU;
+      tb->hc[L] = off + k;
+    } else if (k < nbz + na1) {  // a tap jj: -a_jj y_e(t - jj)
+      const int jj = k - nbz + 1;
+      tb->coef[L] = -s->pl_a[(size_t)e * s->pl_maxa + jj];
+      tb->hoff[L] = kSmEOff + ep * kSmE;
+      tb->hc[L] = jj;
+      tb->hmask[L] = kSmE - 1;
+    }
+  }
+  // A's columns: y part in state order, then MV n's past-control register (age k) at
+  // kSmY + kSmR n + k
+  tb->acol.assign(s->nx, 0);
+  for (int c = 0; c < s->nyh; ++c) tb->acol[c] = c;
+  for (int n = 0; n < s->nu; ++n)
+    for (int k = 0; k < s->dum[n]; ++k) tb->acol[s->upoff[n] + k] = kSmY + kSmR * n + k;
+  return true;
+}
+
 // longest run of numerator taps from each entry's first nonzero one (mdband_kernel.hip keeps only
 // those in LDS: the delay's leading zeros are skipped by pl_off / mz_off anyway)
 static void compact_taps(const mpct_scenario* s, DevScenario& ds) {
@@ -835,6 +884,13 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   size_t o_wsc = put(s->wscale.data(), s->wscale.size() * 8);
   size_t o_xc = put(s->xc.data(), s->xc.size() * 4);
   size_t o_nm = put(s->nm.data(), s->nm.size() * 8);
+  SmallTables smt;
+  const bool small = small_plant(s, &smt);
+  size_t o_smc = put(smt.coef.data(), smt.coef.size() * 8);
+  size_t o_smo = put(smt.hoff.data(), smt.hoff.size() * 4);
+  size_t o_smh = put(smt.hc.data(), smt.hc.size() * 4);
+  size_t o_smm = put(smt.hmask.data(), smt.hmask.size() * 4);
+  size_t o_sma = put(smt.acol.data(), smt.acol.size() * 4);
   void* dp = nullptr;
   if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
   if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -866,6 +922,12 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   ds.pl_maxb = s->pl_maxb;
   ds.pl_maxa = s->pl_maxa;
   ds.regpath = regpath(s);
+  ds.small = small ? 1 : 0;
+  ds.sm_coef = reinterpret_cast<const double*>(b + o_smc);
+  ds.sm_hoff = reinterpret_cast<const int*>(b + o_smo);
+  ds.sm_hc = reinterpret_cast<const int*>(b + o_smh);
+  ds.sm_hmask = reinterpret_cast<const int*>(b + o_smm);
+  ds.sm_acol = reinterpret_cast<const int*>(b + o_sma);
   ds.step = reinterpret_cast<const double*>(b + o_step);
   ds.phi = reinterpret_cast<const double*>(b + o_phi);
   ds.n1 = reinterpret_cast<const int*>(b + o_n1);
@@ -1287,6 +1349,7 @@ extern "C" int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts*
     ds.nx = s->nx;
     ds.dtc = s->dtc;
     ds.regpath = regpath(s);
+    ds.small = small_plant(s) ? 1 : 0;
     nm = closed_loop_instance(ds, s->nu * s->numax, ext);
   }
   if (buf && cap > 0) {
@@ -1315,6 +1378,7 @@ static int64_t lds_bytes_ext(const mpct_scenario* s, int32_t N2, int32_t Nu, boo
   ds.fr_max = s->fr_max;
   ds.mdband = s->mdband;
   ds.regpath = regpath(s);
+  ds.small = small_plant(s) ? 1 : 0;
   ds.my = s->my;
   ds.nd = s->nd;
   compact_taps(s, ds);

@@ -253,11 +253,13 @@ def test_kernel_instance_and_multi_validation(built):
     from mpct.scenarios import shell3x3
 
     sc, r, _ = shell3x3(n2_max=30, nu_max=5)
-    assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,false,false>"
+    # cost-only batches of a small plant run gpc_small_kernel; the open-loop leg the general kernel
+    assert kernel_instance(sc) == "gpc_small_kernel"
     assert kernel_instance(sc, open_loop=True) == "gpc_closed_loop_kernel<16,false,true>"
     sc6, _, _ = shell3x3(n2_max=30, nu_max=6)
     # mixed Nu: every simulation runs in the smallest QP-size class that holds it
-    assert kernel_instance(sc6) == "gpc_closed_loop_kernel<16,false,false> + <32,false,false>"
+    assert kernel_instance(sc6) == "gpc_small_kernel + gpc_closed_loop_kernel<32,false,false>"
+    assert kernel_instance(sc6, want_traj=True) == "gpc_closed_loop_kernel<16,false,true> + <32,false,true>"
     sc15, _, _ = shell3x3(n2_max=127, nu_max=15)
     assert kernel_instance(sc15, want_traj=True) == ("gpc_closed_loop_kernel<16,false,true> + <32,false,true> + "
                                                      "<64,false,true>")

@@ -26,7 +26,7 @@ def test_c_client_builds_and_validates(built):
     out = subprocess.run([_build()], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "expected error: nu*nu_max > 32" in out.stdout and out.stdout.strip().endswith("ok")
-    assert "linear instance gpc_closed_loop_kernel<16,false,false>" in out.stdout
+    assert "linear instance gpc_small_kernel" in out.stdout
 
 
 @pytest.mark.gpu

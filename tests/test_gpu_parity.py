@@ -305,8 +305,8 @@ def test_two_streams_share_a_scenario(env):
 @pytest.fixture(scope="module")
 def metric(built, has_gpu):
     """The benchmark's own scenario: shell3x3(n2_max=30, nu_max=5) -- nu*nu_max = 15, so the
-    cost-only calls launch gpc_closed_loop_kernel<16,false,false> under its VGPR cap (the instance
-    bench.py times), trajectory calls the <16,false,true> instance."""
+    cost-only calls launch gpc_small_kernel (the small-plant kernel bench.py times), trajectory calls
+    the general gpc_closed_loop_kernel<16,false,true> instance."""
     if not has_gpu:
         pytest.skip("no GPU")
     from mpct.engine import kernel_instance
@@ -315,7 +315,7 @@ def metric(built, has_gpu):
     from oracle.scenarios import shell3x3 as o_shell3x3
 
     sc, r, yref = shell3x3(n2_max=30, nu_max=5)
-    assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,false,false>"
+    assert kernel_instance(sc) == "gpc_small_kernel"
     assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<16,false,true>"
     osc, orr, oyref, _ = o_shell3x3()
     return dict(sc=sc, r=r, osc=osc, oyref=oyref, cp=CPort(osc, 30, 500, oyref))

@@ -131,7 +131,7 @@ def test_mex_builds_creates_and_validates(built):
                (1, ["nonsense"])])
     assert res[0][0] and int(res[0][1][0].item()) == _lib.ABI_VERSION
     assert res[1][0] and res[1][1][0].dtype == np.uint64
-    assert res[2][1][0] == "gpc_closed_loop_kernel<16,false,false>"
+    assert res[2][1][0] == "gpc_small_kernel"
     assert res[3][1][0] == "gpc_closed_loop_kernel<16,false,true>"
     assert res[4] == (False, ("mpct:desc", "descriptor field 'yref' is missing"))
     assert not res[5][0] and res[5][1][0] == "mpct:handle"
