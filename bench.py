@@ -185,23 +185,24 @@ def pmc_traffic(C, n2, nu):
     """roofline.traffic from the committed PMC pass (profiles/pmc_latest.json, written by
     tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes) -- accepted only
     when that pass profiled this very library (same sha256) on this workload; otherwise None.
-    Returns (bytes per launch | None, source note)."""
+    Returns (bytes per launch | None, source note, the pass's counter-derived FP64 rate | None)."""
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(pmc):
-        return None, "no PMC pass committed"
+        return None, "no PMC pass committed", None
     try:
         with open(pmc) as f:
             pj = json.load(f)
     except (OSError, ValueError):
-        return None, "unreadable profiles/pmc_latest.json"
+        return None, "unreadable profiles/pmc_latest.json", None
     mine = lib_sha256()
     src = "profiles/%s_pmc.json" % pj.get("tag", "?")
     if pj.get("lib_sha256") != mine:
         return None, "%s profiled libmpct.so sha256 %s, this run loaded %s: not used" % (
-            src, str(pj.get("lib_sha256"))[:16], mine[:16])
+            src, str(pj.get("lib_sha256"))[:16], mine[:16]), None
     if (pj.get("candidates"), pj.get("n2"), pj.get("nu")) != (C, n2, nu):
-        return None, "%s is for another workload: not used" % src
-    return pj.get("hbm_bytes_per_launch"), "%s (PMC pass of this libmpct.so, sha256 %s)" % (src, mine[:16])
+        return None, "%s is for another workload: not used" % src, None
+    return (pj.get("hbm_bytes_per_launch"), "%s (PMC pass of this libmpct.so, sha256 %s)" % (src, mine[:16]),
+            pj.get("fp64_counter"))
 
 
 def cpu_model() -> str:
@@ -329,7 +330,7 @@ def main():
             tdist.destroy_process_group()
         return
 
-    traffic, traffic_source = pmc_traffic(C, args.n2, args.nu)
+    traffic, traffic_source, fp64c = pmc_traffic(C, args.n2, args.nu)
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -389,6 +390,9 @@ def main():
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": kernel_name, "kernel_ms": kms,
                      "algorithmic_gflop_per_launch": fl / 1e9, "qp_iters_per_step": I_as,
+                     # what the SIMDs issued, from the same sha-keyed PMC pass: every
+                     # FP64 VALU wave-instruction at 64 lanes over the rocprof kernel time
+                     "fp64_counter_tflops": fp64c.get("tflops") if fp64c else None,
                      "bound_note": "FP64 vector ALU issue + per-step dependent latency (no MFMA on this path: "
                                    "DESIGN §6); peak = MI355X FP64 vector dense peak"},
         "cpu_baseline": cpu,

@@ -58,7 +58,7 @@ __host__ __device__ inline LdsLayout lds_layout(const DevScenario& sc, int M, bo
   L.jt = take(regqp ? 0 : M * M);  // J of the active-set method, column-major JT[k*M + i] = J(i,k)
   L.dv = take(regqp ? 0 : M);      // d = J'n_p
   L.ra = take(M * M);        // R_A of the active-set method (persists across steps)
-  L.sl = take(4 * M);        // slacks of the 4M constraints at the unconstrained minimiser
+  L.sl = take(regqp ? 0 : 4 * M);  // wide classes: slacks of the 4M constraints at x_u
   L.gb = take(regqp ? 16 * kBS : 0);  // M <= 16 class: B = R_A^-1 (row-major, stride kBS)
   L.A = take(((nx + 1) & ~1) * M);  // row-major A[m][s], rows padded to even length (16-B reads)
   L.x = take(nx + 1);
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
     PSTAMP(PROF_UNC);
     if constexpr (MAXM <= 16) {
       double xq;
-      iters += gi_qp16(lds + L.rinv, lds + L.ra, lds + L.sl, M, Nu, rcn, qrow < M ? suprev[rcn.n] : 0.0, xu,
+      iters += gi_qp16(lds + L.rinv, lds + L.ra, M, Nu, rcn, qrow < M ? suprev[rcn.n] : 0.0, xu,
                        tol, maxit, &st, gis, rf, DTC ? kGiRebuild16Dtc : kGiRebuild16, xq
 #ifdef MPCT_PROFILE
                        , pacc, pprev
@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
 
 namespace mpct {
 
-long long small_lds_bytes(int M);  // gpc_small.hip
+long long small_lds_bytes(const DevScenario& sc, int M);  // gpc_small.hip
 int launch_small(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                  const double* lambda, const double* r, const DevOpts& o, const DevResult& out, const int* perm,
                  int first, hipStream_t stream, std::string* err);
@@ -553,7 +553,7 @@ int launch_small(const DevScenario& sc, long long C, int nref, const int* N2, co
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu, bool ext) {
   (void)N2;
   const int M = sc.nu * Nu;
-  if (sc.small && !ext && M <= 16) return small_lds_bytes(M);
+  if (sc.small && !ext && M <= 16) return small_lds_bytes(sc, M);
   LdsLayout L = lds_layout(sc, M, ext);
   return (long long)L.total * 8;
 }

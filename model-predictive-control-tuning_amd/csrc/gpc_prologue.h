@@ -18,10 +18,11 @@
 
 namespace mpct {
 
-// Outputs in LDS: R (upper, row-major, M x M) in sR; R^-1 (upper, row-major) in sRi; the gain
+// Outputs in LDS: R (upper, row-major, M x M) in sR; R^-1 (upper: row-major M x M, or PACKED its
+// upper triangle row by row, gpc_qp16.h rinv_idx) in sRi; the gain
 // A = -R^-1 T with state column vc of row m at sA[m * astride + acol(vc)] (acol: host column map,
 // nullptr = identity).  Returns false (uniformly) when R is not positive definite.
-template <int MAXM>
+template <int MAXM, bool PACKED = false>
 __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, int M, int Nu, int N2,
                                              const double* dl, const double* lm, double* sR, double* sRi,
                                              double* sA, int astride, const int* acol) {
@@ -150,14 +151,18 @@ __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, in
         if (m < M) sA[m * astride + ac] = -rcol[m];
     }
   }
-  // R^-1 (upper, row-major): lane j solves R x = e_j in its own LDS column (zeros below)
+  // R^-1: lane j solves R x = e_j in its own LDS column (zeros below unless PACKED)
+  auto ri = [&](int i, int k) __attribute__((always_inline)) -> int {
+    return PACKED ? i * M - ((i * (i - 1)) >> 1) + (k - i) : i * M + k;
+  };
   if (lane < M) {
     for (int kk = lane; kk >= 0; --kk) {
       double a = (kk == lane) ? 1.0 : 0.0;
-      for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[j * M + lane];
-      sRi[kk * M + lane] = a / sR[kk * M + kk];
+      for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[ri(j, lane)];
+      sRi[ri(kk, lane)] = a / sR[kk * M + kk];
     }
-    for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
+    if (!PACKED)
+      for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
   }
   lds_sync();
   return true;

@@ -164,16 +164,27 @@ struct BoxMark16 {
   }
 };
 
-// J <- R^-1 (row-major in LDS, upper), B <- 0
+// entry (i, k), k >= i, of the upper-triangular R^-1 in LDS: row-major M x M, or (PACKED) its
+// upper triangle row by row (M (M + 1) / 2 doubles)
+template <bool PACKED>
+__device__ __forceinline__ int rinv_idx(int i, int k, int M) {
+  return PACKED ? i * M - ((i * (i - 1)) >> 1) + (k - i) : i * M + k;
+}
+
+// J <- R^-1 (upper, in LDS), B <- 0 (rows i < M: B has M rows of stride kBS; lanes i >= M only
+// ever read their own rows, whose products no QP row uses)
+template <bool PACKED>
 __device__ __forceinline__ void gi16_load_rinv(GIState<16>& S, RegFactors& F, const double* sRi, int M) {
   const int i = q16_i(), b = q16_b();
   FOR4(r, {
     const int k = 4 * b + r;
-    F.J[r] = (i < M && k < M) ? sRi[i * M + k] : 0.0;
+    F.J[r] = (i < M && k < M && k >= i) ? sRi[rinv_idx<PACKED>(i, k, M)] : 0.0;
   });
-  double2* p = reinterpret_cast<double2*>(F.sB + i * kBS + 4 * b);
-  p[0] = make_double2(0.0, 0.0);
-  p[1] = make_double2(0.0, 0.0);
+  if (i < M) {
+    double2* p = reinterpret_cast<double2*>(F.sB + i * kBS + 4 * b);
+    p[0] = make_double2(0.0, 0.0);
+    p[1] = make_double2(0.0, 0.0);
+  }
   S.nrot = 0;
   S.jinit = true;
 }
@@ -313,9 +324,9 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
 // the QP of one step (M <= 16): unconstrained minimiser xu (row vector), u(t-1) of the row's MV
 // up_row, the row's constraint data rc (both replicated over the four row blocks); the optimal
 // moves come back in xout (row vector, registers; xu itself when it is feasible).  rebuild: the
-// J rebuild interval in units of M rotations (gpc_qp.h)
-template <class Dummy = void>
-__device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, double* ssl, int M, int Nu,
+// J rebuild interval in units of M rotations (gpc_qp.h); PACKED: R^-1's layout (rinv_idx)
+template <bool PACKED = false>
+__device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, int Nu,
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
                                        int* st, GIState<16>& S, RegFactors& F, int rebuild, double& xout
 #ifdef MPCT_PROFILE
@@ -359,14 +370,10 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, double* s
     if (S.q == 0) {
       S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
     } else {
-      if (lane < M) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
-      }
       if (!S.jinit || S.nrot >= rebuild * M) {
         // rebuild J and B for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
-        gi16_load_rinv(S, F, sRi, M);
+        gi16_load_rinv<PACKED>(S, F, sRi, M);
         S.q = 0;
         for (int v = 0; v < qq; ++v) {
           const int p = __builtin_amdgcn_readlane(S.ww, v);
@@ -395,7 +402,15 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, double* s
           xm = xu;
           break;
         }
-        const double c = i < q ? -ssl[S.ww] : 0.0;  // b_A - N_A'x_u
+        // c = b_A - N_A'x_u: lane w < q gathers the slack at x_u of its constraint ww = 4 m + kind
+        // from QP row m (ds_bpermute; no LDS buffer)
+        double c;
+        {
+          const int src = (S.ww >= 0 ? S.ww >> 2 : 0) + 16 * q16_b();
+          const double g0 = __shfl(s[0], src, kWave), g1 = __shfl(s[1], src, kWave);
+          const double g2 = __shfl(s[2], src, kWave), g3 = __shfl(s[3], src, kWave);
+          c = i < q ? -sel4v_v(g0, g1, g2, g3, S.ww & 3) : 0.0;
+        }
         d4v Bl, w;
         b_row4(F.sB, Bl);
         FOR4(r, w[r] = i < q ? Bl[r] * c : 0.0;);
@@ -443,7 +458,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, double* s
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }
-    if (!S.jinit) gi16_load_rinv(S, F, sRi, M);
+    if (!S.jinit) gi16_load_rinv<PACKED>(S, F, sRi, M);
     const int p = bid;
     int j0, mp;
     double sgp;

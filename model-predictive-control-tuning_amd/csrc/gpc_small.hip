@@ -41,21 +41,21 @@
 namespace mpct {
 
 // LDS layout of one simulation (doubles, 16-byte aligned pieces)
+// (the Shell 3x3 metric, M = 15: 10,064 B, so 16 workgroups fit a CU's 160 KB)
 struct SmallLayout {
-  int rinv, ra, sl, gb, A, xy, ring, hist, total;
+  int rinv, ra, gb, A, xy, ring, hist, total;
 };
-__host__ __device__ inline SmallLayout small_layout(int M) {
+__host__ __device__ inline SmallLayout small_layout(const DevScenario& sc, int M) {
   SmallLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
-  L.rinv = take(M * M);             // R^-1 (J rebuilds)
+  L.rinv = take(M * (M + 1) / 2);   // R^-1, packed upper triangle (J rebuilds)
   L.ra = take(M * M);               // R_A (R during the prologue)
-  L.sl = take(4 * M);               // warm-start slacks
-  L.gb = take(16 * kBS);            // B = R_A^-1 (gpc_qp16.h)
-  L.A = take(16 * kSmA);            // A, 16 rows (rows >= M zero) x kSmA columns
+  L.gb = take(M * kBS);             // B = R_A^-1 (gpc_qp16.h), M rows
+  L.A = take(M * kSmA);             // A, M rows x kSmA columns
   L.xy = take(kSmY);                // y part of x
   L.ring = take(3 * 2 * kSmR);      // past-control rings, two copies each
-  L.hist = take(kSmHist);           // plant input rings [nu][kSmU] | entry output rings [16][kSmE]
+  L.hist = take(kSmEOff + 4 * sc.my * sc.sm_ke);  // input rings [3][kSmU] | entry output rings [4 my][ke]
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -68,7 +68,10 @@ __device__ __forceinline__ int sm_lane() {
   return l;
 }
 
-__global__ void __launch_bounds__(64, 3)
+#ifndef MPCT_XP_SMALL_WAVES
+#define MPCT_XP_SMALL_WAVES 3
+#endif
+__global__ void __launch_bounds__(64, MPCT_XP_SMALL_WAVES)
     gpc_small_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
                      const int* __restrict__ Nuv, const double* __restrict__ deltav,
                      const double* __restrict__ lambdav, const double* __restrict__ rv,
@@ -101,14 +104,14 @@ __global__ void __launch_bounds__(64, 3)
   unsigned long long pacc[PROF_N] = {};
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
-  const SmallLayout L = small_layout(M);
+  const SmallLayout L = small_layout(sc, M);
   double* sA = lds + L.A;
   for (int e = lane; e < L.total - L.A; e += kWave) sA[e] = 0.0;  // A pads, state, rings
   lds_sync();
 
   // ------------------------------------------------------------------ prologue (gpc_prologue.h)
-  if (!gpc_prologue<16>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.ra, lds + L.rinv, sA,
-                        kSmA, sc.sm_acol)) {
+  if (!gpc_prologue<16, true>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.ra, lds + L.rinv,
+                              sA, kSmA, sc.sm_acol)) {
     write_nan(MPCT_ST_NONFINITE_);
     return;
   }
@@ -119,6 +122,7 @@ __global__ void __launch_bounds__(64, 3)
   const double pcoef = sc.sm_coef[lane];
   const int pbase = L.hist + sc.sm_hoff[lane];
   const int pc = sc.sm_hc[lane], pmask = sc.sm_hmask[lane];
+  const int ke = sc.sm_ke;
   // output lane 4 i (i < my): y difference state offset and length
   const int oi = (lane >> 2) & 3;
   const int yoff = oi < my ? sc.yoff[oi] : 0;
@@ -149,7 +153,7 @@ __global__ void __launch_bounds__(64, 3)
   rf.sB = lds + L.gb;
   long long iters = 0;
   int st = 0;
-  double yd0 = 0.0, yd1 = 0.0, yd2 = 0.0;  // lane 4 i: nabla^k y_i(t - 1), k = 0..2
+  double yd0 = 0.0;  // lane 4 i: y_i(t - 1)
   double uprev = 0.0;                                 // lane n < nu: u_n(t - 1)
   double j1 = 0.0, j22 = 0.0;
   double r_t = psr[0], yr_t = psy[0];
@@ -162,20 +166,21 @@ __global__ void __launch_bounds__(64, 3)
     const double ye = row4_sum(pcoef * hv);  // y_e(t) on lane e of every row
     double yi = ye + dppd<kQx1>(ye);
     yi += dppd<kQx2>(yi);  // y_i(t) on every lane of quad i
-    if (sm_lane() < 16) lds[L.hist + kSmEOff + sm_lane() * kSmE + (t & (kSmE - 1))] = ye;
+    if (sm_lane() < 4 * my) lds[L.hist + kSmEOff + sm_lane() * ke + (t & (ke - 1))] = ye;
     PSTAMP(PROF_PLANT);
     // ---- y update and costs (lane 4 i): x = [y - r, nabla y, .., nabla^na y] (difference basis)
     {
       const int l = sm_lane();
       if ((l & ~12) == 0 && (l >> 2) < my) {
-        const double n1 = yi - yd0, n2 = n1 - yd1, n3 = n2 - yd2;
+        // nabla^1,2 y(t-1) are the state's own entries of the last step (read before they are
+        // overwritten); y(t-1) stays in a register
         double* xs = lds + L.xy + yoff;
+        const double o1 = xs[1], o2 = xs[2];
+        const double n1 = yi - yd0, n2 = n1 - o1, n3 = n2 - o2;
         xs[0] = yi - r_t;
         if (nyh > 1) xs[1] = n1;
         if (nyh > 2) xs[2] = n2;
         if (nyh > 3) xs[3] = n3;
-        yd2 = n2;
-        yd1 = n1;
         yd0 = yi;
         const double e1 = yi - yr_t;
         j1 = fma(e1, e1, j1);
@@ -196,18 +201,20 @@ __global__ void __launch_bounds__(64, 3)
       const double2* av = reinterpret_cast<const double2*>(lds + aoff);
       const double* xv = lds + xo;
       double a0 = 0.0, a1 = 0.0;
+      if ((sm_lane() & 15) < M) {  // A has M rows
 #pragma unroll
-      for (int p = 0; p < kSmR / 2; ++p) {
-        const double2 a = av[p];
-        a0 = fma(a.x, xv[2 * p], a0);
-        a1 = fma(a.y, xv[2 * p + 1], a1);
-      }
-      if (sm_lane() < 16) {
-#pragma unroll
-        for (int p = kSmR / 2; p < kSmY / 2; ++p) {
+        for (int p = 0; p < kSmR / 2; ++p) {
           const double2 a = av[p];
           a0 = fma(a.x, xv[2 * p], a0);
           a1 = fma(a.y, xv[2 * p + 1], a1);
+        }
+        if (sm_lane() < 16) {
+#pragma unroll
+          for (int p = kSmR / 2; p < kSmY / 2; ++p) {
+            const double2 a = av[p];
+            a0 = fma(a.x, xv[2 * p], a0);
+            a1 = fma(a.y, xv[2 * p + 1], a1);
+          }
         }
       }
       xu = row4_sum(a0 + a1);  // row m of A x on lanes m, m+16, m+32, m+48 (0 for m >= M)
@@ -216,7 +223,7 @@ __global__ void __launch_bounds__(64, 3)
     // ---- QP (gpc_qp16.h): u(t-1) of the row's MV from lane n
     double xq;
     const double up_row = __shfl(uprev, rcn.n, kWave);
-    iters += gi_qp16(lds + L.rinv, lds + L.ra, lds + L.sl, M, Nu, rcn, up_row, xu, tol, maxit, &st, gis, rf,
+    iters += gi_qp16<true>(lds + L.rinv, lds + L.ra, M, Nu, rcn, up_row, xu, tol, maxit, &st, gis, rf,
                      kGiRebuild16, xq
 #ifdef MPCT_PROFILE
                      , pacc, pprev
@@ -262,7 +269,7 @@ __global__ void __launch_bounds__(64, 3)
 
 namespace mpct {
 
-long long small_lds_bytes(int M) { return (long long)small_layout(M).total * 8; }
+long long small_lds_bytes(const DevScenario& sc, int M) { return (long long)small_layout(sc, M).total * 8; }
 
 // the M <= 16 class of a cost-only batch on a small scenario (launch_closed_loop); first: this
 // launch also writes the statuses of skipped / bad-horizon candidates
@@ -270,7 +277,7 @@ int launch_small(const DevScenario& sc, long long C, int nref, const int* N2, co
                  const double* lambda, const double* r, const DevOpts& o, const DevResult& out, const int* perm,
                  int first, hipStream_t stream, std::string* err) {
   const int nu_cls = sc.numax < 16 / sc.nu ? sc.numax : 16 / sc.nu;
-  const long long lds = small_lds_bytes(sc.nu * nu_cls);
+  const long long lds = small_lds_bytes(sc, sc.nu * nu_cls);
   const long long S = C * nref;
   hipLaunchKernelGGL(gpc_small_kernel, dim3((unsigned)S), dim3(kWave), (size_t)lds, stream, sc, C, nref, N2, Nu,
                      delta, lambda, r, perm, o, out, first);

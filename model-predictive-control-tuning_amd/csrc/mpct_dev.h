@@ -37,9 +37,8 @@ constexpr int kSmY = 12;                   // y difference state: columns of A's
 constexpr int kSmR = 8;                    // past-control ring per MV: columns of quarters 1..3
 constexpr int kSmA = kSmY + 3 * kSmR;      // A row stride
 constexpr int kSmU = 16;                   // plant input ring per MV (power of two, > longest delay + taps)
-constexpr int kSmE = 4;                    // plant entry output ring (power of two, > denominator taps)
-constexpr int kSmEOff = 3 * kSmU;          // entry output rings after the input rings
-constexpr int kSmHist = kSmEOff + 16 * kSmE;
+constexpr int kSmE = 4;                    // longest plant entry output ring (power of two > denominator taps)
+constexpr int kSmEOff = 3 * kSmU;          // entry output rings (4 my of them) after the input rings
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
 constexpr int MPCT_ST_QP_MAXITER_ = 1;
@@ -68,6 +67,7 @@ struct DevScenario {
   // plant term of lane L = 16 k + 4 i + j (coefficient, history ring offset in the kernel's history
   // region, delay, ring mask) and the state column -> A column map
   int small;
+  int sm_ke;              // entry output ring length (DevScenario::small scenarios: 2 or 4)
   const double* sm_coef;  // [64]
   const int* sm_hoff;     // [64]
   const int* sm_hc;       // [64]
@@ -169,5 +169,11 @@ inline StageRow stage_row(const DevResult& o, int my, int nu) {
 // section ids of the diagnostic in-kernel stamps
 enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,
        PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_QWARM, PROF_N = 13 };
+// nmpc_kernel.hip's sections (same slots): the prediction with tangents and its streamed QR when
+// it starts an iteration, R^-1 and the unconstrained step, the QP, the Anderson candidate's
+// prediction, the full-step (alpha = 1) trial prediction, the shorter Armijo trials (tangent-free),
+// the plant's RK4 step, everything else
+enum { PROF_NM_FULL = 0, PROF_NM_RINV, PROF_NM_QP, PROF_NM_AA, PROF_NM_LS0, PROF_NM_TRIAL, PROF_NM_PLANT,
+       PROF_NM_OTHER };
 
 }  // namespace mpct

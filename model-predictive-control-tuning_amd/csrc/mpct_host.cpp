@@ -760,6 +760,7 @@ static int regpath(const mpct_scenario* s) {
 // my <= 4 outputs, nu <= 3 MVs, no MD / plant-only inputs, one plant, GPC mode, y difference state
 // <= kSmY entries (<= 4 per output), past-control registers <= kSmR, <= 4 plant terms per entry
 struct SmallTables {
+  int ke = 2;
   std::vector<double> coef;
   std::vector<int> hoff, hc, hmask, acol;
 };
@@ -775,6 +776,9 @@ static bool small_plant(const mpct_scenario* s, SmallTables* tb = nullptr) {
     if (nbz + na1 > 4 || na1 >= kSmE || s->pl_nb[e] > kSmU) return false;
   }
   if (!tb) return true;
+  int na_max = 0;
+  for (int e = 0; e < s->ne; ++e) na_max = std::max(na_max, s->pl_na[e] - 1);
+  tb->ke = na_max < 2 ? 2 : 4;  // entry output ring: a power of two above the denominator taps
   tb->coef.assign(kWave, 0.0);
   tb->hoff.assign(kWave, 0);
   tb->hc.assign(kWave, 0);
@@ -791,9 +795,9 @@ static bool small_plant(const mpct_scenario* s, SmallTables* tb = nullptr) {
     } else if (k < nbz + na1) {  // a tap jj: -a_jj y_e(t - jj)
       const int jj = k - nbz + 1;
       tb->coef[L] = -s->pl_a[(size_t)e * s->pl_maxa + jj];
-      tb->hoff[L] = kSmEOff + ep * kSmE;
+      tb->hoff[L] = kSmEOff + ep * tb->ke;
       tb->hc[L] = jj;
-      tb->hmask[L] = kSmE - 1;
+      tb->hmask[L] = tb->ke - 1;
     }
   }
   // A's columns: y part in state order, then MV n's past-control register (age k) at
@@ -923,6 +927,7 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   ds.pl_maxa = s->pl_maxa;
   ds.regpath = regpath(s);
   ds.small = small ? 1 : 0;
+  ds.sm_ke = smt.ke;
   ds.sm_coef = reinterpret_cast<const double*>(b + o_smc);
   ds.sm_hoff = reinterpret_cast<const int*>(b + o_smo);
   ds.sm_hc = reinterpret_cast<const int*>(b + o_smh);
@@ -1055,8 +1060,11 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
         sum[k] += (double)hp[i * PROF_N + k];
         mx[k] = std::max(mx[k], (double)hp[i * PROF_N + k]);
       }
-    const char* nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
-                              "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm"};
+    const char* gpc_nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
+                                  "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm"};
+    const char* nmpc_nm[PROF_N] = {"full_pass", "rinv+step", "qp", "anderson_pass", "ls_full_pass", "ls_trials",
+                                   "plant_rk4", "other", "-", "-", "-", "-", "-"};
+    const char** nm = s->nmpc ? nmpc_nm : gpc_nm;
     fprintf(stderr, "[mpct profile] mean / max cycles per simulation over %lld sims\n", S);
     for (int k = 0; k < PROF_N; ++k)
       fprintf(stderr, "  %-14s %12.0f %12.0f\n", nm[k], sum[k] / (double)S, mx[k]);
@@ -1378,7 +1386,11 @@ static int64_t lds_bytes_ext(const mpct_scenario* s, int32_t N2, int32_t Nu, boo
   ds.fr_max = s->fr_max;
   ds.mdband = s->mdband;
   ds.regpath = regpath(s);
-  ds.small = small_plant(s) ? 1 : 0;
+  {
+    SmallTables smt;
+    ds.small = small_plant(s, &smt) ? 1 : 0;
+    ds.sm_ke = smt.ke;
+  }
   ds.my = s->my;
   ds.nd = s->nd;
   compact_taps(s, ds);

@@ -228,6 +228,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
   const int N = Nv[c], Nu = Nuv[c];
   const int M = nu * Nu;
   int st = 0;
+#ifdef MPCT_PROFILE
+  // diagnostic build: section cycle sums (tools/nmpc_latency.py --profile; labels: mpct_host.cpp)
+  unsigned long long pacc[PROF_N] = {};
+  unsigned long long pprev = __builtin_amdgcn_s_memtime();
+#endif
 
   auto write_nan = [&](int status) __attribute__((always_inline)) {
     if (lane < ny) {
@@ -451,9 +456,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
     double fcur = 0.0;
     for (int it = 0; it < sc.sqp_max; ++it) {
       ++sqp_total;
+      PSTAMP(PROF_NM_OTHER);
       if (!have) {
         bool xin_;
         fcur = full_pass(v, xin_);
+        PSTAMP(PROF_NM_FULL);
       }
       have = false;
       const double f0 = fcur;
@@ -472,6 +479,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
       double xm = 0.0;
       if (row)
         for (int k = lane; k < M; ++k) xm -= sRi[lane * M + k] * scv[k];
+      PSTAMP(PROF_NM_RINV);
       // ---- box QP: lb <= U + cumulative step <= ub, Goldfarb-Idnani from s_u
       const double clo = row ? lbn - sU[lane] : 0.0, chi = row ? ubn - sU[lane] : 0.0;
       lds_sync();
@@ -570,6 +578,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
           break;
         }
       }
+      PSTAMP(PROF_NM_QP);
       // ---- convergence on the absolute-move change of the full step (oracle: max|d|/s_u)
       const double dpre = block_prefix<MAXM>(xm, bl, Nu, row, sxc);
       double chg = row ? fabs(dpre) / sun : 0.0;
@@ -604,7 +613,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
           const double upl = lane_prev<MAXM>(ucl);
           const double vc = row ? (bl == 0 ? ucl - ulb : ucl - upl) : 0.0;
           bool xin;
+          PSTAMP(PROF_NM_OTHER);
           const double fc = full_pass(vc, xin);
+          PSTAMP(PROF_NM_AA);
           if (xin && fc <= f0 + kLsC1 * dd) {
             v = vc;
             taken = true;
@@ -625,7 +636,10 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
         bool xin;
         // the full step's trial is a full pass (usually taken), shorter steps a tangent-free one
         const double va = v + (row ? alpha * xm : 0.0);
+        PSTAMP(PROF_NM_OTHER);
         const double f1 = ls == 0 ? full_pass(va, xin) : trial(va, xin);
+        if (ls == 0) PSTAMP(PROF_NM_LS0);
+        else PSTAMP(PROF_NM_TRIAL);
         if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
           if (ls == 0) {
             have = true;
@@ -688,7 +702,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
       lds_sync();
       double un[2] = {ul[0] + sxc[0], nu > 1 ? ul[1] + sxc[Nu] : 0.0};
       lds_sync();
+      PSTAMP(PROF_NM_OTHER);
       vdv_rk4<false>(P, h, nsub, x, un, nullptr, nullptr);
+      PSTAMP(PROF_NM_PLANT);
       ul[0] = un[0];
       ul[1] = un[1];
       // warm start for the next step: the solution shifted by one move (last move repeated),
@@ -726,6 +742,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
     }
   }
   if (!inb) st |= MPCT_ST_BOUNDS_;
+#ifdef MPCT_PROFILE
+  PSTAMP(PROF_NM_OTHER);
+  if (lane == 0 && out.prof)
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+#endif
   // ------------------------------------------------------------------ results
   if (lane < ny) {
     if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;

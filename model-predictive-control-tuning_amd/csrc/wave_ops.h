@@ -17,7 +17,9 @@ __device__ __forceinline__ void lds_sync() {
   // one-wave workgroup: LDS requests of a wave complete in order; wait for this lane's and order
   // the compiler's memory operations around the hand-off
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#ifndef MPCT_XP_NOWAIT
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+#endif
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 

@@ -182,8 +182,12 @@ class Scenario:
         return buf
 
     def dims(self) -> dict:
-        k = ["my", "nu", "nd", "n2_max", "nu_max", "tlen", "nx", "nyh", "nup"]
-        return dict(zip(k, self.table(2).astype(int).tolist()))
+        """mpct_scenario_table(2): the ABI-6 dims table, every entry named."""
+        k = ["my", "nu", "nd", "n2_max", "nu_max", "tlen", "nx", "nyh", "nup", "nit", "nq"]
+        t = self.table(2)
+        if t.size != len(k):
+            raise MpctError("dims table has %d entries, expected %d" % (t.size, len(k)))
+        return dict(zip(k, t.astype(int).tolist()))
 
     def lds_bytes(self, N2=None, Nu=None, costs_only=False) -> int:
         """LDS per workgroup with the open-loop leg / trajectories (or, costs_only, of the

@@ -5,6 +5,7 @@ vns_objective VNS2.m:147-195   — F for a batch of (N, Nu) neighbours at fixed 
              plants: one simulation per output, VNS2.m:148-165; non-square: one simulation with
              Xsp, VNS2.m:166-169); measured disturbances Par.mdv are passed to every simulation
              (VNS2.m:153,168, GAM_fun.m:81)
+vns_row1_broadcast  VNS2.m:172-195 with only row 1 of Xy assigned (implicit expansion)
 precon       PreCon.m:23-27
 failed       which statuses make a simulation unusable (the reference's swallowed exception)
 rank         stable ranking of candidates (primary cost, candidate-index tiebreak)
@@ -99,6 +100,23 @@ def vns_objective(sc, N2, Nu, delta, lam, inK=10, device=-1, refs=None, mdv=None
         j21, j22, jnu = res.j21, res.j22, res.Jnu
     F = j21.sum(1) + j22.sum(1) + N2 + jnu.sum(1)
     return F, j21, j22, jnu, res
+
+
+def vns_row1_broadcast(sc, N2, Nu, delta, lam, inK=10, device=-1, refs=None, mdv=None) -> float:
+    """VNS2.m:172-195 when Xy holds only row 1 (a square plant's simulations of outputs 2..my have
+    all failed so far in this VNS2 pass, VNS2.m:151-163): errYref = Xy - Yref broadcasts row 1
+    against every output's Yref (MATLAB implicit expansion), j21 and Jnu stay scalars, so
+    sum(j21 + j22) + sum(Jnu) = my j21_1 + sum_i sum_{t >= inK} (y_1(t) - Yref_i(t))^2 + Jnu_1.
+    Returns that (F without N(1)) from simulation 1 (output 1 stepped) with its trajectory."""
+    refs = vns_step_refs(sc.my, sc.nit, inK) if refs is None else np.asarray(refs, dtype=float)
+    refs = refs.reshape(-1, sc.my, sc.nit)[:1]
+    v = None if mdv is None or np.size(mdv) == 0 else np.asarray(mdv, dtype=float)[None]
+    res = eval_batch(sc, np.array([N2], np.int32), np.array([Nu], np.int32),
+                     np.asarray(delta, dtype=float).reshape(1, sc.my), np.asarray(lam, dtype=float).reshape(1, sc.nu),
+                     refs, v=v, open_loop=True, want_traj=True, device=device)
+    y1 = res.y[0, 0, inK - 1:]
+    B = ((y1[None, :] - np.asarray(sc.yref, dtype=float)[:, inK - 1:]) ** 2).sum(1)
+    return float(sc.my * res.j21[0, 0] + B.sum() + res.Jnu[0, 0])
 
 
 def rank(cost) -> np.ndarray:

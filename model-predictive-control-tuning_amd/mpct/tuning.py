@@ -202,10 +202,16 @@ class StaleRows:
     (:172-195) mixes rows of different neighbours.  Row i enters F only through
     T_i = j21_i + j22_i + Jnu_i, so the state is the last T per row.  The rows are never
     initialised: MATLAB zero-fills rows below an assigned one (T_i0 = sum_{t >= inK} Yref_i(t)^2:
-    Xy = Xyma = Xuma = 0), and while fewer than my rows exist :173 (Xy - Yref) throws, which
-    ends the reference's run; here that neighbour scores NaN (never taken).
-    score(N1, terms, ok) -> F = sum_i T_i + N(1) with terms = T of this neighbour's simulations
-    and ok = which of them succeeded; call reset() at the start of every VNS2 pass."""
+    Xy = Xyma = Xuma = 0).
+    While only row 1 exists (every earlier simulation of outputs 2..my failed), :173
+    Xy - Yref broadcasts the 1 x K row against the my x K Yref (implicit expansion), and
+    F = my j21_1 + sum_i sum_{t >= inK} (y_1 - Yref_i)^2 + N(1) + Jnu_1: the evaluator supplies
+    that quantity without N(1) as a callable ``bcast`` of row 1's simulation (evaluated lazily;
+    objectives.vns_row1_broadcast).  With 1 < rows < my the expansion fails and :173 throws,
+    which ends the reference's run; here that neighbour scores NaN (never taken), as it does with
+    one row when no ``bcast`` is given.
+    score(N1, terms, ok[, bcast]) -> F with terms = T of this neighbour's simulations and ok =
+    which of them succeeded; call reset() at the start of every VNS2 pass."""
 
     def __init__(self, init_terms):
         self.init = np.asarray(init_terms, dtype=float)
@@ -214,14 +220,21 @@ class StaleRows:
     def reset(self):
         self.last = self.init.copy()
         self.nrows = 0
+        self.row1 = None  # bcast of the simulation that last set row 1
 
-    def score(self, N1, terms, ok):
+    def score(self, N1, terms, ok, bcast=None):
         terms = np.asarray(terms, dtype=float)
         ok = np.asarray(ok, dtype=bool)
         self.last[ok] = terms[ok]
+        if ok[0]:
+            self.row1 = bcast
         if ok.any():
             self.nrows = max(self.nrows, int(np.nonzero(ok)[0].max()) + 1)
         if self.nrows < self.last.size:
+            if self.nrows == 1 and self.row1 is not None:
+                if callable(self.row1):
+                    self.row1 = float(self.row1())
+                return self.row1 + N1
             return math.nan
         return float(self.last.sum()) + N1
 
@@ -251,8 +264,7 @@ def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512
             key = (N, Nu)
             if key in cache:
                 if stale is not None:
-                    terms, ok = cache[key]
-                    return stale.score(N[0], terms, ok)
+                    return stale.score(N[0], *cache[key])
                 return cache[key]
             if key not in pending and len(pending) < max_batch:
                 pending.append(key)
@@ -492,7 +504,7 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None, md
     (GAM_fun.m:81, VNS2.m:153,168).  Only fatal statuses (objectives.FATAL_STATUS: the reference's
     sim would have thrown) score NaN; iteration caps keep their finite cost."""
     from .engine import eval_batch
-    from .objectives import failed, vns_objective
+    from .objectives import failed, vns_objective, vns_row1_broadcast
 
     my, ny = par.my, par.ny
     v = None if mdv is None or np.size(mdv) == 0 else np.asarray(mdv, dtype=float)[None]
@@ -524,11 +536,16 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None, md
         return np.where(bad.any(axis=1), np.nan, F)
 
     def batch_vns_rows(keys, delta, lam):
-        """Square plants: per neighbour (T, ok) with T_i = j21_i + j22_i + Jnu_i of simulation i
-        and ok_i = simulation i succeeded, for StaleRows (VNS2.m:151-163)."""
+        """Square plants: per neighbour (T, ok, bcast) with T_i = j21_i + j22_i + Jnu_i of
+        simulation i, ok_i = simulation i succeeded and bcast the row-1 broadcast F term (lazy),
+        for StaleRows (VNS2.m:151-173)."""
         F, j21, j22, jnu, bad = vns_terms(keys, delta, lam)
         T = j21 + j22 + jnu
-        return [(T[k], ~bad[k]) for k in range(len(keys))]
+
+        def bcast(key):
+            return lambda: vns_row1_broadcast(sc, max(key[0]), max(key[1]), delta, lam, device=device,
+                                              refs=vns_refs, mdv=mdv)
+        return [(T[k], ~bad[k], bcast(keys[k])) for k in range(len(keys))]
 
     batch_vns.rows = batch_vns_rows if my == ny else None
     return batch_j1, batch_vns

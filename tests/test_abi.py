@@ -47,7 +47,8 @@ def test_abi_v1_descriptor_accepted(built, monkeypatch):
     _lib.load()
     monkeypatch.setattr(_lib, "ABI_VERSION", 1)
     sc, r, yref = shell3x3(n2_max=10, nu_max=2)
-    assert sc.dims()["nx"] == 35
+    d = sc.dims()
+    assert d["nx"] == 35 and d["nit"] == 500 and d["nq"] == 0  # every dims entry named
 
 
 def test_mdband_scenario(built, monkeypatch):

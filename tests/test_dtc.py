@@ -189,3 +189,42 @@ def test_config4_range_against_oracle(gpu):
     pairs = [(c, (5 * c + j * 11) % D) for c in range(len(idx)) for j in range(3)]
     worst = _oracle_compare(res, len(idx), D, N2, Nu, d, l, pairs, plants)
     print("config-4 range: %d pairs, max traj rel err %.2e" % (len(pairs), worst))
+
+
+@pytest.mark.gpu
+def test_config4_full_size_properties(gpu):
+    """the launch the dtc-mc bench times, at full size -- the seeded 10,000
+    config-4 candidates x 32 plant-mismatch draws (320,000 closed loops, DTC_GPC_WW.m:18-19 /
+    WoodBerry.m:34-42 draws) in one call, cost only.  Size-independent properties: statuses are
+    only 0 or 4 (the unconstrained DTC loop has no QP; a draw the mismatch destabilises is
+    non-finite), the costs are finite exactly where the status is 0, a repeated launch is bitwise
+    identical, and scoring the candidates in reversed order gives the same per-simulation bits."""
+    import torch
+    from mpct.dtc import config4_candidates, robust_scores, woodberry_mc
+    from mpct.engine import eval_batch_device
+
+    C, D = 10000, 32
+    sc, refs, v, _ = woodberry_mc(draws=D, n2_max=30, nu_max=10)
+    N2, Nu, d, l = config4_candidates(C)
+    dev = torch.device("cuda", 0)
+
+    def run(perm):
+        t = [torch.from_numpy(np.ascontiguousarray(a[perm])).to(dev) for a in (N2, Nu, d, l)]
+        out = dict(J1=torch.empty((C * D, 2), dtype=torch.float64, device=dev),
+                   status=torch.empty(C * D, dtype=torch.int32, device=dev))
+        eval_batch_device(sc, *t, torch.from_numpy(refs).to(dev), out, v=torch.from_numpy(v).to(dev))
+        torch.cuda.synchronize(dev)
+        return out["J1"].cpu().numpy().reshape(C, D, 2), out["status"].cpu().numpy().reshape(C, D)
+
+    ident = np.arange(C)
+    J1, st = run(ident)
+    assert set(np.unique(st).tolist()) <= {0, 4}, np.unique(st)
+    assert np.all(np.isfinite(J1[st == 0])) and (st == 0).mean() > 0.5
+    J1b, stb = run(ident)
+    assert np.array_equal(st, stb) and np.array_equal(J1.view(np.int64), J1b.view(np.int64))
+    rev = ident[::-1]
+    J1r, str_ = run(rev)
+    assert np.array_equal(st, str_[::-1]) and np.array_equal(J1.view(np.int64), J1r[::-1].view(np.int64))
+    mean, worst = robust_scores(np.where(np.isfinite(J1), J1, np.inf).reshape(C * D, 2), C, D)
+    print("config 4 full size: %d of %d closed loops non-finite; best worst-case %.4g"
+          % (int((st == 4).sum()), C * D, float(np.min(worst))))

@@ -66,3 +66,23 @@ def test_short_mpc_tuning_run(env, tmp_path):
     assert np.all(delta > 0) and np.all(lam > 0)
     m = loadmat(p, squeeze_me=True, struct_as_record=False)["Tuning_Parameters"]
     assert int(m.N) == int(np.max(N))
+
+
+def test_vns_row1_broadcast_matches_cport(env):
+    """ADVICE r3 (VNS2.m:172-195 with only row 1 of Xy): my j21_1 + sum_i sum_{t >= inK}
+    (y_1 - Yref_i)^2 + Jnu_1 from the engine's trajectory against the C port's trajectory."""
+    from mpct.objectives import vns_row1_broadcast
+    from oracle.cport import CPort
+    from oracle.scenarios import shell3x3 as o_shell3x3, vns_step_refs
+
+    sc, r, yref = env[:3]
+    osc, orr, oyref, fx = o_shell3x3()
+    cp = CPort(osc, 127, 500, oyref)
+    d, l = np.asarray(fx["delta"]), np.asarray(fx["lambda"])
+    g = vns_row1_broadcast(sc, 24, 6, d, l)
+    res = cp.eval(np.array([24], np.int32), np.array([6], np.int32), d[None], l[None],
+                  np.asarray(vns_step_refs(3, 500))[:1], open_loop=True, want_traj=True)
+    y1 = res["y"][0, 0, 9:]
+    ref = 3 * res["j21"][0, 0] + ((y1[None] - np.asarray(oyref)[:, 9:]) ** 2).sum() + res["Jnu"][0, 0]
+    assert np.isfinite(g)
+    np.testing.assert_allclose(g, ref, rtol=1e-6)

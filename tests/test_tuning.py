@@ -350,6 +350,31 @@ def test_vns_stale_rows_semantics():
     np.testing.assert_allclose(stale_rows_for(Y).init, [11.0, 4.0 * 11])
 
 
+def test_vns_stale_rows_one_row_broadcasts():
+    """with only row 1 of Xy assigned, VNS2.m:173 Xy - Yref broadcasts (implicit
+    expansion) and F is finite: the row-1 simulation's broadcast term (lazy, evaluated once) plus
+    N(1), kept while later neighbours' row-1 simulations fail; with 1 < rows < my it throws."""
+    from mpct.tuning import StaleRows
+
+    calls = []
+
+    def bc(v):
+        def f():
+            calls.append(v)
+            return v
+        return f
+
+    s = StaleRows([10.0, 20.0, 30.0])
+    assert s.score(5, [1, 2, 3], [True, False, False], bc(100.0)) == 105.0
+    assert s.score(6, [4, 5, 6], [False, False, False], bc(7.0)) == 106.0   # row 1 stale: its term
+    assert s.score(6, [4, 5, 6], [True, False, False], bc(200.0)) == 206.0  # row 1 replaced
+    assert calls == [100.0, 200.0]
+    assert math.isnan(s.score(6, [4, 5, 6], [False, True, False], bc(1.0)))  # two rows: throws
+    assert s.score(6, [4, 5, 6], [False, False, True], bc(1.0)) == 4 + 5 + 6 + 6
+    s.reset()
+    assert math.isnan(s.score(5, [1, 2, 3], [True, False, False]))  # no broadcast term given
+
+
 def test_vns2_batched_stale_rows_equals_sequential():
     """The speculative batched VNS with stale-row scoring takes the sequential search's decisions:
     a synthetic square plant where some neighbours' simulations fail."""

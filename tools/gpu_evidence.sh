@@ -2,7 +2,8 @@
 # One end-of-round evidence pass on the GPU box (repo root): the -m gpu suite, smoke(), the bench
 # line, a rocprofv3 --kernel-trace --stats pass, separate FETCH_SIZE and WRITE_SIZE passes (for
 # roofline.traffic, keyed to this libmpct.so's sha256), and one SQ pass with the LDS bank-conflict
-# counters.  Each GPU step has its own time limit; the first failure ends the script.
+# counters plus a second SQ pass (FP64 ADD / MUL / TRANS, SALU, wait states) for
+# roofline.fp64_counter_tflops.  Each GPU step has its own time limit; the first failure ends the script.
 # Usage: bash tools/gpu_evidence.sh TAG   -> gpurun_out/TAG/
 set -eo pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"
@@ -22,4 +23,6 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o write -- "${BENCH[@]}" > "$O/write.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_FMA_F64 \
   --output-format csv -d "$O/sq" -o sq -- python3 "$R/tools/ab.py" > "$O/sq.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  --output-format csv -d "$O/sq2" -o sq2 -- python3 "$R/tools/ab.py" > "$O/sq2.log" 2>&1
 echo evidence done

@@ -18,7 +18,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "gpc_closed_loop_kernel"
+KERNEL = "gpc_small_kernel"  # the metric's timed instance (--kernel for another)
 
 
 def counter(path, name):
@@ -35,7 +35,9 @@ def main():
     ap.add_argument("--candidates", type=int, default=4096)
     ap.add_argument("--n2", type=int, default=30)
     ap.add_argument("--nu", type=int, default=5)
+    ap.add_argument("--kernel", default=KERNEL)
     a = ap.parse_args()
+    globals()["KERNEL"] = a.kernel
     src = os.path.join(ROOT, "gpurun_out", a.tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -60,22 +62,31 @@ def main():
         # bench.py uses hbm_bytes_per_launch only when the library it loads has this hash
         "lib_sha256": open(os.path.join(src, "lib_sha256.txt")).read().split()[0],
     }
-    sqd = os.path.join(src, "sq")
-    if os.path.isdir(sqd):  # tools/gpu_evidence.sh: SQ instruction mix and LDS bank conflicts
-        import glob
-        agg = {}
-        for f in glob.glob(os.path.join(sqd, "*counter_collection.csv")):
+    import glob
+    agg = {}
+    for sub in ("sq", "sq2"):  # tools/gpu_evidence.sh: two SQ passes (8 SQ counters each)
+        for f in glob.glob(os.path.join(src, sub, "*counter_collection.csv")):
             for r in csv.DictReader(open(f)):
                 if KERNEL in r["Kernel_Name"]:
                     agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if agg:
         med = {k: statistics.median(v) for k, v in agg.items()}
         steps = a.candidates * 500.0
         out["sq"] = {"per_launch_median": med,
-                     "per_sim_step": {k: med[k] / steps for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS",
-                                                                  "SQ_INSTS_VALU_FMA_F64", "SQ_WAVE_CYCLES") if k in med},
+                     "per_sim_step": {k: med[k] / steps for k in sorted(med) if k.startswith("SQ_INSTS")
+                                      or k == "SQ_WAVE_CYCLES"},
                      "lds_bank_conflict_per_lds_active": med.get("SQ_LDS_BANK_CONFLICT", 0.0) /
                      max(med.get("SQ_LDS_IDX_ACTIVE", 1.0), 1.0),
                      "note": "SQ_WAVE_CYCLES in quad-cycles (MI355X_MICROARCH.md); tools/ab.py batch"}
+        f64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64")
+        if all(k in med for k in f64) and avg_ns:
+            # every issued FP64 VALU wave-instruction counted at 64 lanes (FMA = 2 flops): the FP64
+            # rate the SIMDs issued, an upper bound on lane-level FP64 work (masked lanes count)
+            fl = 64.0 * (2.0 * med[f64[0]] + med[f64[1]] + med[f64[2]])
+            out["fp64_counter"] = {"flops_issued_per_launch": fl,
+                                   "tflops": fl / (avg_ns * 1e-9) / 1e12,
+                                   "trans_f64_per_launch": med.get("SQ_INSTS_VALU_TRANS_F64"),
+                                   "formula": "64 x (2 FMA_F64 + ADD_F64 + MUL_F64) / rocprof kernel time"}
     for name in (a.tag + "_pmc.json", "pmc_latest.json"):
         with open(os.path.join(dst, name), "w") as f:
             json.dump(out, f, indent=1)

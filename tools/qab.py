@@ -1,6 +1,7 @@
 """Kernel time of the Shell 3x3 metric batch at several batch sizes (HIP events, median of 5) for
 the library in MPCT_LIB (default libmpct.so; variant builds: tools/variant.sh).
-Usage: python tools/qab.py [C ...]   (hC: the C candidates of the 4096 grid with the most QP work)"""
+Usage: python tools/qab.py [C ...]   (hC: the C candidates of the 4096 grid with the most QP work;
+QAB_DUMP=f.npz saves the 4096 batch's J1 and QP iterations for a bitwise comparison of builds)"""
 import os
 import sys
 
@@ -41,5 +42,7 @@ for arg in sys.argv[1:] or ["1024", "4096", "8192"]:
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
+    if os.environ.get("QAB_DUMP") and arg == "4096":  # bitwise A/B of variant builds
+        np.savez(os.environ["QAB_DUMP"], J1=out["J1"].cpu().numpy(), it=out["qp_iters"].cpu().numpy())
     print("%s C=%6s kernel ms: median %.3f min %.3f  (%.0f sims/s) status nz %d" % (
         tag, arg, np.median(ts), min(ts), C / np.median(ts) * 1e3, int((out["status"] != 0).sum())), flush=True)
