@@ -29,25 +29,27 @@
 #include "launch_fan.h"
 #include "mpct_dev.h"
 
+#ifndef MPCT_XP_POLISH_K
+#define MPCT_XP_POLISH_K 1
+#endif
+#ifndef MPCT_XP_DRIFT_K
+#define MPCT_XP_DRIFT_K 4
+#endif
+
 namespace mpct {
 
 struct BandLayout {
   int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, plb, pla,
-      mzb, mza, step, total;
+      mzb, mza, total;
 };
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
-#ifndef MPCT_BAND_CAPS_KB
-#define MPCT_BAND_CAPS_KB 26, 32, 40, 53, 80, 160  // LDS tiers of the class launches: 6/5/4/3/2/1 workgroups per CU
-                                               // (the last must be 160; tools/ab3.sh: 4 tiers 3.09 s, these 2.88 s)
-#endif
-#ifndef MPCT_BAND_STEP_L2
-#define MPCT_BAND_STEP_L2 1  // the QP reads the MV step table from global memory (L1/L2-resident, shared by every
-                             // simulation) instead of an LDS copy: 21.5 KB less LDS at N2 = 127, 3.14 -> 3.09 s
-#endif
-// LDS copy of the MV step table: samples 0..N2 of each entry, row stride tls
-__host__ __device__ inline int band_tls(const DevScenario& sc, int N2) { return sc.tlen < N2 + 1 ? sc.tlen : N2 + 1; }
+// LDS tiers of the class launches: 6/5/4/3/2/1 workgroups per CU (the last must be 160;
+// tools/ab3.sh: 4 tiers 3.09 s, these 2.88 s).  The QP reads the MV step table from global memory
+// (L1/L2-resident, shared by every simulation) instead of an LDS copy: 21.5 KB less LDS at
+// N2 = 127, 3.14 -> 3.09 s
+constexpr long long kBandCapsKb[] = {26, 32, 40, 53, 80, 160};
 
 // full_ri: R^-1 is a full triangle (some OV weight > 0); in band mode R is diagonal and only its
 // inverse diagonal is kept.  ncopy: 2 with the open-loop prediction (a second plant copy), else 1
@@ -80,7 +82,6 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.pla = take(ne * sc.pl_maxa);
   L.mzb = take(ne * sc.mz_maxbc);
   L.mza = take(ne * sc.mz_maxa);
-  L.step = take(MPCT_BAND_STEP_L2 ? 0 : my * nu * band_tls(sc, N2));
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -152,7 +153,7 @@ __global__ void __launch_bounds__(64, 1)
   const BandLayout L = band_layout(sc, N2, M, any_q, o.open_loop ? 2 : 1);
   // this launch serves one (QP size, LDS) class: the others' simulations leave at once
   if (Mz <= mz_lo || Mz > MAXM || (long long)L.total * 8 <= lds_lo || (long long)L.total * 8 > lds_hi) return;
-  const int tls = MPCT_BAND_STEP_L2 ? sc.tlen : band_tls(sc, N2);
+  const int tls = sc.tlen;
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
@@ -176,19 +177,9 @@ __global__ void __launch_bounds__(64, 1)
   double* spla = lds + L.pla;
   double* smzb = lds + L.mzb;
   double* smza = lds + L.mza;
-#if MPCT_BAND_STEP_L2
-  const double* __restrict__ sstep = sc.step;
-#else
-  double* sstep = lds + L.step;
-#endif
+  const double* __restrict__ sstep = sc.step;  // global, L1/L2-resident
 
   // ------------------------------------------------------------------ prologue
-#if !MPCT_BAND_STEP_L2
-  for (int e = lane; e < my * nu * tls; e += kWave) {
-    const int en = e / tls;
-    sstep[e] = sc.step[en * tlen + (e - en * tls)];
-  }
-#endif
   for (int e = lane; e < ne * sc.pl_maxbc; e += kWave) {
     const int en = e / sc.pl_maxbc, l = e - en * sc.pl_maxbc, off = sc.pl_off[en];
     splb[e] = off + l < sc.pl_nb[en] ? sc.pl_b[en * sc.pl_maxb + off + l] : 0.0;
@@ -474,7 +465,7 @@ __global__ void __launch_bounds__(64, 1)
         for (int k = 0; k < 4; ++k) ssl[4 * lane + k] = s[k];
       }
       lds_sync();
-      if (force || !gis.jinit || gis.nrot >= 4 * Mz) {
+      if (force || !gis.jinit || gis.nrot >= MPCT_XP_DRIFT_K * Mz) {
         const int qq = gis.q;
         load_j();
         gis.q = 0;
@@ -554,7 +545,7 @@ __global__ void __launch_bounds__(64, 1)
       if (!(best < -tol)) {
         // optimal up to the incremental updates: after a long QP re-solve the final active set
         // exactly from x_u (fresh J) and re-check every row before accepting
-        if (gis.q > 0 && gis.nrot >= Mz && npolish < 2) {
+        if (gis.q > 0 && gis.nrot >= MPCT_XP_POLISH_K * Mz && npolish < 2) {
           ++npolish;
           xm = recentre(true);
           continue;
@@ -566,7 +557,7 @@ __global__ void __launch_bounds__(64, 1)
         st |= MPCT_ST_QP_MAXITER_;
         break;
       }
-      if (gis.q > 0 && gis.nrot >= 4 * Mz) {  // J has drifted: rebuild it and re-centre x
+      if (gis.q > 0 && gis.nrot >= MPCT_XP_DRIFT_K * Mz) {  // J has drifted: rebuild it and re-centre x
         xm = recentre(true);
         continue;
       }
@@ -869,8 +860,8 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
     return -4;
   }
   auto kern = mdband_closed_loop_kernel<MAXM>;
-  static const long long capkb[] = {MPCT_BAND_CAPS_KB};  // workgroups per CU: 160 KB / cap
-  constexpr int kCaps = (int)(sizeof(capkb) / sizeof(capkb[0]));
+  const long long* capkb = kBandCapsKb;  // workgroups per CU: 160 KB / cap
+  constexpr int kCaps = (int)(sizeof(kBandCapsKb) / sizeof(kBandCapsKb[0]));
   static_assert(kCaps <= 8, "at most 8 LDS tiers");
   long long lo[8], hi[8];
   int ncls = 0;

@@ -53,30 +53,6 @@ __device__ __forceinline__ VdV vdv_load(const double* p) {
   return P;
 }
 
-#ifndef MPCT_RHS_FAST
-#define MPCT_RHS_FAST 1  // 1: 1/th by v_rcp_f64 + Newton (config 5: 326 -> 293 ms); 2: also exp by exp_estrin
-                         // (306 ms: more VALU than the libm exp, 2 % lower small-batch latency); 0: libm
-#endif
-
-// exp(x): Cody-Waite reduction by ln 2 (hi part with 32 trailing zero bits, so n*ln2_hi is exact),
-// degree-13 Taylor polynomial on |r| <= ln2/2 (truncation < 5e-18) by Estrin's scheme (dependency
-// depth 4 instead of Horner's 13), then 2^n by v_ldexp_f64.  Within 2 ulp of the correctly
-// rounded value; overflow -> inf and underflow -> 0 through ldexp.
-__device__ __forceinline__ double exp_estrin(double x) {
-  const double n = __builtin_rint(x * 1.4426950408889634074);
-  const double r = fma(-n, 1.90821492927058770002e-10, fma(-n, 6.93147180369123816490e-01, x));
-  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-  const double q0 = fma(r, 1.0, 1.0);
-  const double q1 = fma(r, 1.0 / 6.0, 0.5);
-  const double q2 = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  const double q3 = fma(r, 1.0 / 5040.0, 1.0 / 720.0);
-  const double q4 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0);
-  const double q5 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0);
-  const double q6 = fma(r, 1.0 / 6227020800.0, 1.0 / 479001600.0);
-  const double s0 = fma(q1, r2, q0), s1 = fma(q3, r2, q2), s2 = fma(q5, r2, q4);
-  const double t0 = fma(s1, r4, s0), t1 = fma(q6, r4, s2);
-  return __builtin_ldexp(fma(t1, r8, t0), (int)n);
-}
 
 // state derivative f(x, u) (nmpc_vandevusse_state.m:64-82) and, with TAN, its directional
 // derivative along (xd, ud)
@@ -85,22 +61,13 @@ __device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const d
                                         const double ud[2], double f[3], double fd[3]) {
   const double ca = x[0], cb = x[1], T = x[2];
   const double th = T + 273.15;
-#if MPCT_RHS_FAST >= 1
+  // 1/th by v_rcp_f64 + two Newton steps (config 5: 326 -> 293 ms, profiles/r02i_nmpc_rhs_ab.txt);
+  // an Estrin-scheme exp measured 306 ms (more VALU than the libm exp) and is not kept
   const double ith = rcp_nr(th);
-#else
-  const double ith = 1.0 / th;
-#endif
-#if MPCT_RHS_FAST >= 2
-  const double ex1 = exp_estrin(P.e1 * ith);
-  const double k1 = P.k10 * ex1;
-  const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp_estrin(P.e2 * ith));  // E1 = E2 in the reference model
-  const double k3 = P.k30 * exp_estrin(P.e3 * ith);
-#else
   const double ex1 = exp(P.e1 * ith);
   const double k1 = P.k10 * ex1;
   const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp(P.e2 * ith));  // E1 = E2 in the reference model
   const double k3 = P.k30 * exp(P.e3 * ith);
-#endif
   const double fov = u[0], tk = u[1];
   f[0] = fov * (P.ca0 - ca) - k1 * ca - k3 * ca * ca;
   f[1] = -fov * cb + k1 * ca - k2 * cb;
@@ -201,15 +168,10 @@ struct StateMark {
   }
 };
 
-#ifndef MPCT_NMPC_WAVES16
-#define MPCT_NMPC_WAVES16 1  // VGPR budget of the M <= 16 class, in waves per SIMD: 2 or 3 spill and ran config 5
-#endif                       // 27 % slower (1 wave: 342 VGPRs; profiles/r02i_nmpc_code_size.txt)
-#ifndef MPCT_NMPC_WAVES32
-#define MPCT_NMPC_WAVES32 1
-#endif
-
+// one wave per SIMD (342 VGPRs): capped at 2 or 3 waves the kernel spills and config 5 ran 27 %
+// slower (profiles/r02i_nmpc_code_size.txt)
 template <int MAXM>
-__global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 32 ? MPCT_NMPC_WAVES32 : 1))
+__global__ void __launch_bounds__(64, 1)
     nmpc_closed_loop_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ Nv,
                             const int* __restrict__ Nuv, const double* __restrict__ deltav,
                             const double* __restrict__ lambdav, const double* __restrict__ rv,
@@ -772,14 +734,11 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_NMPC_WAVES16 : (MAXM <= 
 
 #include "work_order.h"
 
-#ifndef MPCT_NMPC_CAPS16_KB
-#define MPCT_NMPC_CAPS16_KB 13  // M <= 16 class: 12 workgroups per CU up to 13 KB, the rest above
-#endif
-#ifndef MPCT_NMPC_CAPS32_KB
-#define MPCT_NMPC_CAPS32_KB 32  // M <= 32 class: 5 workgroups per CU up to 32 KB, the rest above
-#endif
-
 namespace mpct {
+
+// LDS tiers (KB) of the class launches: M <= 16 class 12 workgroups per CU up to 13 KB, M <= 32
+// class 5 up to 32 KB, the rest above (finer tiers measured slower)
+constexpr long long kNmCap16Kb = 13, kNmCap32Kb = 32;
 
 long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
 
@@ -794,9 +753,9 @@ static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int
   const int Mhi = std::min(sc.nu * sc.numax, MAXM);
   const long long lds_max = nmpc_lds_bytes(Mhi, sc.n2max);
   // LDS tiers (KB) of the class launches; the last one takes the rest up to lds_max
-  static const long long c16[] = {MPCT_NMPC_CAPS16_KB}, c32[] = {MPCT_NMPC_CAPS32_KB};
+  static const long long c16[] = {kNmCap16Kb}, c32[] = {kNmCap32Kb};
   const long long* caps = MAXM <= 16 ? c16 : c32;
-  const int ncap = MAXM <= 16 ? (int)(sizeof(c16) / sizeof(c16[0])) : (int)(sizeof(c32) / sizeof(c32[0]));
+  const int ncap = 1;
   long long lo[8], hi[8];
   int ncls = 0;
   for (long long l = 0; ncls < 8 && l < lds_max; ++ncls) {

@@ -124,10 +124,7 @@ __device__ __forceinline__ double qsum(double v) {
     return wave_sum64(v);
   }
 }
-#ifndef MPCT_PACKED_ARGMIN
-#define MPCT_PACKED_ARGMIN 1  // M <= 16 argmin on one order-preserving 64-bit key (value bits | id)
-#endif
-// (v, id) -> one unsigned key whose order is v's order, with v's low 6 mantissa bits replaced by
+// M <= 16 argmin on one order-preserving 64-bit key (value bits | id): (v, id) -> one unsigned key whose order is v's order, with v's low 6 mantissa bits replaced by
 // id (< 64): one u64 compare per DPP step instead of the (value, id) pair.  The winner's exact
 // value is re-read from its lane (ids are 4 * lane + k or lane: lane = id >> shift).
 __device__ __forceinline__ unsigned long long argkey(double v, int id) {
@@ -152,7 +149,7 @@ __device__ __forceinline__ unsigned long long row_minkey(unsigned long long k) {
 template <int MAXM>
 __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
   if constexpr (MAXM <= 16) {
-    if (MPCT_PACKED_ARGMIN && shift >= 0) {
+    if (shift >= 0) {
       // lanes >= 16 hold INF (callers), so row 0's minimum is the QP rows' minimum
       const unsigned long long k = row_minkey(argkey(v, id));
       const int kid = (int)(__builtin_amdgcn_readlane((int)(unsigned)k, 0) & 63);

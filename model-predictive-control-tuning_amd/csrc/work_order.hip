@@ -4,16 +4,6 @@
 #include "wave_ops.h"
 #include "work_order.h"
 
-#ifndef MPCT_GPC_EST
-#define MPCT_GPC_EST 1  // GPC / DTC-GPC batches keyed by order_keys_gpc (0: the weight-ratio key)
-#endif
-#ifndef MPCT_NMPC_KEY
-#define MPCT_NMPC_KEY 1  // NMPC dispatch key: 1 N Nu; 2 N Nu, then the weight ratio; 0 log(N Nu) - 0.1 a
-                         // (config 5 GAM mode: 267 / 267 / 288 ms, tools/diag/nmpc_order_ab.py)
-#endif
-#ifndef MPCT_KEY_SKIP
-#define MPCT_KEY_SKIP 0  // ablation bits of order_keys_gpc: 1 H build, 2 Cholesky, 4 jump scan
-#endif
 
 namespace mpct {
 
@@ -31,7 +21,7 @@ namespace mpct {
 // iteration grows with the horizon N and the QP size.  Since the Anderson-accelerated iteration
 // (round 2), N Nu alone orders the batch as well as the measured work (GAM mode: 267 ms for both,
 // grid order 331 ms); the round-1 score log(N Nu) - 0.1 a, which also weighed the iteration
-// count, now costs 288 ms (MPCT_NMPC_KEY).
+// count, measured 288 ms (tools/diag/nmpc_order_ab.py) and is not kept.
 __global__ void order_keys(int kind, long long C, int my, int nu, const int* __restrict__ N2,
                            const int* __restrict__ Nu, const double* __restrict__ delta,
                            const double* __restrict__ lambda, unsigned* __restrict__ key, int* __restrict__ idx) {
@@ -46,17 +36,8 @@ __global__ void order_keys(int kind, long long C, int my, int nu, const int* __r
     double a = 0.0;
     for (int j = 0; j < nu; ++j) a += log2(fmax(dmax, 1e-300) / fmax(fabs(lambda[c * nu + j]), 1e-300));
     a /= nu;
-    if (kind == kOrderNmpc && MPCT_NMPC_KEY == 0) {
-      // heavier = larger score; map the float score to an order-preserving unsigned, inverted
-      const float sc = (float)(log((double)n2 * nuc) - 0.1 * a);
-      unsigned u = __float_as_uint(sc);
-      u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-      k = ~u;
-    } else if (kind == kOrderNmpc) {
-      // N * Nu first (the prediction's length times the QP size), then, with MPCT_NMPC_KEY 2,
-      // the smaller weight ratio first (more Gauss-Newton iterations)
-      const double qa = MPCT_NMPC_KEY == 2 ? fmin(fmax((256.0 - a) * 32.0, 0.0), 16383.0) : 0.0;
-      k = ~(((unsigned)(n2 * nuc) << 14) | (unsigned)qa);
+    if (kind == kOrderNmpc) {
+      k = ~((unsigned)(n2 * nuc) << 14);  // N * Nu: the prediction's length times the QP size
     } else {
       const double qd = fmin(fmax((a + 256.0) * 2048.0, 0.0), 1048575.0);
       const unsigned M = (unsigned)(nu * nuc);
@@ -118,11 +99,6 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
       ++a;
     }
     b += a;
-#if MPCT_KEY_SKIP & 1
-    sH[a * M + b] = a == b ? 1.0 : 0.0;
-    sH[b * M + a] = a == b ? 1.0 : 0.0;
-    continue;
-#endif
     const int na = a / nuc, la = a - na * nuc, nb = b / nuc, lb = b - nb * nuc;
     const int lm = la > lb ? la : lb;
     double h = 0.0;
@@ -164,7 +140,7 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   // trailing block; no integer division in the loop)
   bool spd = true;
   const bool hr = lane < M;
-  for (int k = 0; k < ((MPCT_KEY_SKIP & 2) ? 0 : M); ++k) {
+  for (int k = 0; k < M; ++k) {
     const double pk = sH[k * M + k];
     if (!(pk > 0.0)) {
       spd = false;
@@ -233,7 +209,7 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     // move) pairs add |z| / b_n, b_n = half the tighter of MV n's rate and amplitude ranges (an
     // unbounded MV adds nothing)
     double e = 0.0;
-    for (int k = 0; k < ((MPCT_KEY_SKIP & 4) ? 0 : nref); ++k) {
+    for (int k = 0; k < nref; ++k) {
       const double* rk = r + (long long)k * my * nit;
       for (int t0 = 1; t0 < nit; t0 += kWave) {
         const int t = t0 + lane;
@@ -319,7 +295,7 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   const size_t lds = sc ? (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) *
                                   sizeof(double) + (size_t)sc->my * sizeof(int)
                         : 0;
-  if (MPCT_GPC_EST && kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && Mp <= 64 &&
+  if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && Mp <= 64 &&
       hcost <= kOrderEstMaxCost && lds <= 64 * 1024) {
     hipLaunchKernelGGL(order_keys_gpc, dim3((unsigned)C), dim3(kWave), lds, stream, *sc, C, nref, N2, Nu, delta,
                        lambda, r, kin, iin);
