@@ -68,10 +68,11 @@ __device__ __forceinline__ int sm_lane() {
   return l;
 }
 
-#ifndef MPCT_XP_SMALL_WAVES
-#define MPCT_XP_SMALL_WAVES 3
-#endif
-__global__ void __launch_bounds__(64, MPCT_XP_SMALL_WAVES)
+// four waves per SIMD: 128 VGPRs (one plant coefficient spilled and re-read per step) and 10 KB of
+// LDS, so 16 workgroups fit a CU and the metric's 4096 simulations run in one round.  Against three
+// waves: bitwise the same results, 3.11-3.19 against 3.38-3.46 ms at 8192 candidates, the same
+// 2.21-2.24 ms at 4096 (profiles/r04b_small_ab.txt)
+__global__ void __launch_bounds__(64, 4)
     gpc_small_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
                      const int* __restrict__ Nuv, const double* __restrict__ deltav,
                      const double* __restrict__ lambdav, const double* __restrict__ rv,

@@ -15,11 +15,11 @@ namespace mpct {
 // wave helpers
 __device__ __forceinline__ void lds_sync() {
   // one-wave workgroup: LDS requests of a wave complete in order; wait for this lane's and order
-  // the compiler's memory operations around the hand-off
+  // the compiler's memory operations around the hand-off.  The wait is not needed for
+  // correctness (a fence-only build gave bitwise the same metric grid) and costs nothing
+  // measurable (profiles/r04b_small_ab.txt), so it stays as the conservative form
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#ifndef MPCT_XP_NOWAIT
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
-#endif
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 

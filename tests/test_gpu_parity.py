@@ -154,6 +154,11 @@ def test_full_grid_properties(env):
     assert np.array_equal(rank(a.J1 @ w), rank(ref["J1"] @ w))
 
 
+# simulations of test_dispatch_key_mixed_horizons_and_step_refs whose status differs from the C
+# port's (QP iteration caps on degenerate active sets, rounding-sensitive), per reference count
+KEY_TEST_STATUS_MISMATCH = {1: [], 3: []}
+
+
 def test_dispatch_key_mixed_horizons_and_step_refs(built):
     """The controller-based dispatch key (work_order.hip order_keys_gpc) runs for batches of >= 256
     candidates. Cover both of its solve paths: lanes over (output, move) when my*M <= 64, and one
@@ -176,6 +181,7 @@ def test_dispatch_key_mixed_horizons_and_step_refs(built):
     sc, r, yref = shell3x3(n2_max=30, nu_max=8, nit=150)
     osc, orr, oyref, _ = o_shell3x3()
     cp = CPort(osc, 30, 150, np.ascontiguousarray(oyref[:, :150]))
+    mismatches = {}
     for refs, orefs in ((r[None], orr[None, :, :150]), (vns_step_refs(3, 150), vns_step_refs(3, 150))):
         res = eval_batch(sc, N2, Nu, d, l, refs)
         rev = eval_batch(sc, N2[::-1].copy(), Nu[::-1].copy(), d[::-1].copy(), l[::-1].copy(), refs)
@@ -190,10 +196,15 @@ def test_dispatch_key_mixed_horizons_and_step_refs(built):
         # capped simulation of 960, tools/diag/qr_status_ab.py); compare the ones clean on both
         cst = np.asarray(ref["status"]).reshape(C, -1)
         ok = np.all(st == 0, axis=1) & np.all(cst == 0, axis=1)
-        assert ok[3:].mean() > 0.96, ok[3:].mean()
+        # pin WHICH simulations differ in status from the C port (not a fraction)
+        mism = sorted(int(k) for k in np.nonzero(np.any(st != cst, axis=1))[0] if k >= 3)
+        capped = sorted(int(k) for k in np.nonzero(np.any(st == 1, axis=1))[0])
+        print("refs %d: status mismatches vs C port %s; capped on the device %s" % (refs.shape[0], mism, capped))
+        mismatches[refs.shape[0]] = mism
         a = res.J1.reshape(C, -1)[ok]
         b = np.asarray(ref["J1"]).reshape(C, -1)[ok]
         assert _rel(a, b) < COST_RTOL, _rel(a, b)
+    assert mismatches == KEY_TEST_STATUS_MISMATCH, mismatches
 
 
 def test_rank_device_matches_stable_sort(built):
