@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(64, 1)
   GIState<MAXM> gis;
   gi_reset<MAXM>(gis);
 #ifdef MPCT_DEBUG_BAND
-  int dbg_t = -1;
+  int dbg_t = -1, dbg_reb = 0, dbg_pol = 0, dbg_git = 0;
 #endif
 
   // J = R^-1 (gi_load_rinv), or its diagonal in band mode
@@ -481,6 +481,9 @@ __global__ void __launch_bounds__(64, 1)
           ++it;
         }
         gis.nrot = 0;
+#ifdef MPCT_DEBUG_BAND
+        ++dbg_reb;
+#endif
       }
       lds_sync();
       double x = row ? xu : 0.0;
@@ -547,6 +550,9 @@ __global__ void __launch_bounds__(64, 1)
         // exactly from x_u (fresh J) and re-check every row before accepting
         if (gis.q > 0 && gis.nrot >= MPCT_XP_POLISH_K * Mz && npolish < 2) {
           ++npolish;
+#ifdef MPCT_DEBUG_BAND
+          ++dbg_pol;
+#endif
           xm = recentre(true);
           continue;
         }
@@ -612,6 +618,9 @@ __global__ void __launch_bounds__(64, 1)
     }
     if (row) sxc[lane] = xm;
     lds_sync();
+#ifdef MPCT_DEBUG_BAND
+    dbg_git = git;
+#endif
     return it;
   };
 
@@ -771,12 +780,13 @@ __global__ void __launch_bounds__(64, 1)
     lds_sync();
 #ifdef MPCT_DEBUG_BAND
     dbg_t = t;
+    dbg_reb = dbg_pol = dbg_git = 0;
     const int it_dbg = solve(Fc, r_t);
     iters += it_dbg;
     if (sim == 0 && lane == 0 && t == MPCT_DEBUG_BAND - 3)
       for (int m = 0; m < Mz; ++m) printf("X %d %.17e\n", m, sxc[m]);
     if (sim == 0 && lane == 0 && t < MPCT_DEBUG_BAND)
-      printf("t=%d it=%d q=%d eps=%.9e du=%.9e %.9e %.9e F0=%.9e Fend=%.9e y6=%.9e st=%d\n", t, it_dbg, gis.q,
+      printf("t=%d it=%d git=%d reb=%d pol=%d q=%d eps=%.9e du=%.9e %.9e %.9e F0=%.9e Fend=%.9e y6=%.9e st=%d\n", t, it_dbg, dbg_git, dbg_reb, dbg_pol, gis.q,
              sxc[M], sxc[0], sxc[Nu], sxc[2 * Nu], Fc[0], Fc[N2 - 1], Fc[6 * N2], st);
 #else
     iters += solve(Fc, r_t);

@@ -253,9 +253,6 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
                      const DevScenario* sc, int nref, const double* r) {
   *perm = nullptr;
-#ifdef MPCT_ORDER_IDENTITY  // probe builds: dispatch in the caller's order
-  return 0;
-#endif
   if (C < kOrderMinC) return 0;  // one round of workgroups: the order cannot matter
   if (wo.pending && hipStreamWaitEvent(stream, wo.used, 0) != hipSuccess) {
     *err = "hipStreamWaitEvent failed (dispatch-order buffers)";
