@@ -153,7 +153,7 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
     qargmin<MAXM>(best, bid, 2);
     PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
-    if (it >= maxit || S.q >= M) {
+    if (it >= maxit) {  // a full active set is legal (a dual step follows, gpc_qp16.h)
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }

@@ -454,7 +454,10 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
     qargmin<16>(best, bid, 2);
     PSTAMP(PROF_QCHECK);
     if (!(best < -tol)) break;
-    if (it >= maxit || S.q >= M) {
+    // a full active set (S.q == M) is legal: beta = 0 there, so the step is a dual one (a drop).
+    // Warm starts reach it whenever every move sits on a bound; bailing out there flagged QPs the
+    // cold-started C port solves (tests/test_gpu_parity.py KEY_TEST_STATUS_MISMATCH)
+    if (it >= maxit) {
       *st |= MPCT_ST_QP_MAXITER_;
       break;
     }

@@ -32,14 +32,17 @@
 #ifndef MPCT_XP_POLISH_K
 #define MPCT_XP_POLISH_K 1
 #endif
+// J is rebuilt and x re-centred after MPCT_XP_DRIFT_K x Mz rotations.  16 against 4 with the
+// normalised constraint choice: config-3 grid 1.67 against 1.70 s, slowest simulation 189 against
+// 198 ms, F beyond 1e-6 of the C port 2.04 against 2.19 % (profiles/r04f_config3_ab.jsonl)
 #ifndef MPCT_XP_DRIFT_K
-#define MPCT_XP_DRIFT_K 4
+#define MPCT_XP_DRIFT_K 16
 #endif
 
 namespace mpct {
 
 struct BandLayout {
-  int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, plb, pla,
+  int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, rn, plb, pla,
       mzb, mza, total;
 };
 
@@ -78,6 +81,7 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.uring = take(ncopy * nin * kURing);
   L.tail = take(ne * kYeHist);  // model entry tails of the window
   L.sext = take(ne);            // model entry window extensions
+  L.rn = take(my * N2);         // output rows' inverse norms: 2 floats (upper, lower) per row
   L.plb = take(ne * sc.pl_maxbc);  // compact: taps from the first nonzero one
   L.pla = take(ne * sc.pl_maxa);
   L.mzb = take(ne * sc.mz_maxbc);
@@ -243,10 +247,15 @@ __global__ void __launch_bounds__(64, 1)
       }
     }
     double* sR = sJT;  // R parks in J's region until the QP starts
+    double hmm = 0.0;  // H(m, m) = |column m of R|^2 (QR keeps W's column norms)
     if (row) {
 #pragma unroll
       for (int k = 0; k < MAXM; ++k)
-        if (k < Mz) sR[k * Mz + lane] = rcol[k];
+        if (k < Mz) {
+          sR[k * Mz + lane] = rcol[k];
+          hmm = fma(rcol[k], rcol[k], hmm);
+        }
+      snv[lane] = 1.0 / hmm;  // D^2 = diag(H)^-1 (the oracle's equilibration, toolbox_band.py band_qp)
     }
     lds_sync();
     bool spd = true;
@@ -267,6 +276,37 @@ __global__ void __launch_bounds__(64, 1)
         sRi[kk * Mz + lane] = a / sR[kk * Mz + kk];
       }
       for (int kk = lane + 1; kk < Mz; ++kk) sRi[kk * Mz + lane] = 0.0;
+    }
+    lds_sync();
+  }
+
+  // the most violated constraint is chosen in the oracle's metric (toolbox_band.py band_qp,
+  // oracle/cband.c): equilibrated variables D^-1 z, D = diag(H)^-1/2, and unit constraint rows,
+  // i.e. the slack over |n o D|.  Raw slacks favour the output rows' large step-response
+  // normals over the move bounds; the heaviest config-3 simulation took 3.5x the oracle's GI steps.
+  // Box rows of lane m: kinds 0/1 (n = e_m), the cumulative kinds 2/3 (n = e_j0 + .. + e_m), eps >= 0
+  // on lane M; output rows q = 2 g + side (upper, lower) from a float table (a selection weight only)
+  double ib01 = 0.0, ib23 = 0.0;
+  const float* srn = reinterpret_cast<const float*>(lds + L.rn);
+  {
+    const double d2 = row ? snv[lane] : 0.0;
+    const double pre = block_prefix<MAXM>(d2, rcn.l, Nu, lane < M, sxc);
+    if (row) {
+      ib01 = rsq_nr(d2);
+      ib23 = lane < M ? rsq_nr(pre) : 0.0;
+    }
+    float* wrn = reinterpret_cast<float*>(lds + L.rn);
+    for (int g = lane; g < P; g += kWave) {
+      const int i = g / N2, k = g - i * N2;
+      const int lmax = min(Nu - 1, k + 1);
+      double a = 0.0;
+      for (int n = 0; n < nu; ++n) {
+        const double* sp = sstep + (i * nu + n) * tls + (k + 1);
+        for (int l = 0; l <= lmax; ++l) a = fma(sp[-l] * sp[-l], snv[n * Nu + l], a);
+      }
+      const double vu = sob[3 * my + i], vl = sob[2 * my + i], de = snv[M];
+      wrn[2 * g] = (float)rsq_nr(fma(vu * vu, de, a));
+      wrn[2 * g + 1] = (float)rsq_nr(fma(vl * vl, de, a));
     }
     lds_sync();
   }
@@ -421,13 +461,17 @@ __global__ void __launch_bounds__(64, 1)
       box_slacks(xm, s);
       if (row) sxc[lane] = xm;
       lds_sync();
-      best = INFINITY;
+      // key = slack / |n o D| over the rows violated beyond tol; best = the winner's raw slack
+      double key = INFINITY;
       bid = 0x7fffffff;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if ((all_rows || !((gis.act >> k) & 1u)) && s[k] < best) {
-          best = s[k];
-          bid = 4 * lane + k;
+        if ((all_rows || !((gis.act >> k) & 1u)) && s[k] < -tol) {
+          const double kk = s[k] * (k < 2 ? ib01 : ib23);
+          if (kk < key) {
+            key = kk;
+            bid = 4 * lane + k;
+          }
         }
       const double eps = sxc[M];
       for (int g = lane; g < P; g += kWave) {
@@ -436,21 +480,36 @@ __global__ void __launch_bounds__(64, 1)
         if (isfinite(sob[my + i])) {
           const int q = 2 * g;
           const double s_up = sob[my + i] + sob[3 * my + i] * eps - yh;
-          if (s_up < best && (all_rows || !out_active(q))) {
-            best = s_up;
-            bid = base + q;
+          if (s_up < -tol && (all_rows || !out_active(q))) {
+            const double kk = s_up * (double)srn[q];
+            if (kk < key) {
+              key = kk;
+              bid = base + q;
+            }
           }
         }
         if (isfinite(sob[i])) {
           const int q = 2 * g + 1;
           const double s_lo = yh - sob[i] + sob[2 * my + i] * eps;
-          if (s_lo < best && (all_rows || !out_active(q))) {
-            best = s_lo;
-            bid = base + q;
+          if (s_lo < -tol && (all_rows || !out_active(q))) {
+            const double kk = s_lo * (double)srn[q];
+            if (kk < key) {
+              key = kk;
+              bid = base + q;
+            }
           }
         }
       }
-      wave_argmin64(best, bid);
+      wave_argmin64(key, bid);
+      if (key == INFINITY) {
+        best = INFINITY;
+      } else if (bid < base) {  // the winner's raw slack: a box row of lane bid >> 2
+        const int k = bid & 3;
+        const double sv = k == 0 ? s[0] : (k == 1 ? s[1] : (k == 2 ? s[2] : s[3]));
+        best = bcast(sv, bid >> 2);
+      } else {
+        best = out_slack(F, bid - base, eps);
+      }
     };
     int it = 0;   // all factorisation work (GI steps + rebuild re-adds + re-centring drops): qp_iters
     int git = 0;  // GI add/drop steps only: the iteration cap guards against cycling, not rebuilds

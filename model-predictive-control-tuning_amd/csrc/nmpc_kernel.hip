@@ -125,31 +125,55 @@ constexpr int kLsMax = 12;
 constexpr double kLsC1 = 1e-4;
 constexpr double kLsFlat = 1e-14;
 
-// LDS layout (doubles) of one simulation at QP size M
+// lane groups of the multi-point prediction pass: the M <= 15 class runs up to four
+// points of one controller call at once, one per 16-lane DPP row (the pass is bound by the FP64
+// issue of one wave, not by its lanes); the M <= 32 class runs one
+template <int MAXM>
+constexpr int kNmRows = MAXM <= 16 ? 4 : 1;
+
+// LDS layout (doubles) of one simulation at QP size M with G point buffers
 struct NmLayout {
-  int ri, jt, ra, rr, dv, xc, u, uo, rw, cv, nv, bits, xp, sx, total;
+  int ri, jt, ra, dv, xc, uo, nv, bits, grp, gsz, total;
+  // offsets inside one point buffer: R, c = Q'r, absolute moves, increments, rate residuals,
+  // predicted states, their sensitivities
+  int g_rr, g_cv, g_u, g_v, g_rw, g_xp, g_sx;
 };
-// N: prediction horizon (the state-bound rows: predicted states x_i and dx_i/dv, i = 1..N)
-__host__ __device__ inline NmLayout nm_layout(int M, int N) {
+// N: prediction horizon (the state-bound rows: predicted states x_i and dx_i/dv, i = 1..N).
+// G: point buffers (nm_groups)
+__host__ __device__ inline NmLayout nm_layout(int M, int N, int G) {
   NmLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.ri = take(M * M);
   L.jt = take(M * M);
   L.ra = take(M * M);
-  L.rr = take(M * M);  // R of the Gauss-Newton least-squares QR (row-major, upper)
   L.dv = take(M + 1);
   L.xc = take(M + 1);
-  L.u = take(M + 1);   // absolute moves of the current iterate
   L.uo = take(M + 1);  // absolute moves of the open-loop solution (Info.MVopt)
-  L.rw = take(M + 1);  // rate residuals w_u v of the current iterate
-  L.cv = take(M + 1);  // c = Q'r, the rotated residual
   L.nv = take(M + 1);  // staged normal of a state-bound row
   L.bits = take((6 * N + 63) / 64);  // active state-bound rows (32-bit words)
-  L.xp = take(3 * N);  // predicted states x_i (i = 1..N) of the current iterate
-  L.sx = take(3 * N * M);  // their sensitivities dx_i/dv, row i*3 + s
+  const int w = G > 1 ? 16 : M + 1;  // per-lane vectors of a point (16-lane rows when grouped)
+  int g = 0;
+  auto gtake = [&](int n) { int r = g; g += (n + 1) & ~1; return r; };
+  L.g_rr = gtake(M * M);  // R of the Gauss-Newton least-squares QR (row-major, upper)
+  L.g_cv = gtake(w);
+  L.g_u = gtake(w);
+  L.g_v = gtake(w);
+  L.g_rw = gtake(w);
+  L.g_xp = gtake(3 * N);
+  L.g_sx = gtake(3 * N * M);
+  L.gsz = g;
+  L.grp = o;
+  o += G * g;
   L.total = (o + 1) & ~1;
   return L;
+}
+
+// point buffers of a simulation: four (one per 16-lane row) when they fit 40 KB, i.e. four
+// workgroups per CU, the one-wave-per-SIMD occupancy of this kernel; else two; the M <= 32 class one
+__host__ __device__ inline int nm_groups(int M, int N) {
+  if (M > 15) return 1;
+  return nm_layout(M, N, 4).total * 8 <= 40 * 1024 ? 4 : 2;
 }
 
 // active flags: box rows (p < base) in the lanes' act bits, state-bound rows in an LDS bitmap
@@ -217,23 +241,31 @@ __global__ void __launch_bounds__(64, 1)
     if (first) write_nan(MPCT_ST_BADHORIZON_);
     return;
   }
-  if (M <= mz_lo || M > MAXM) return;  // another launch's QP size class
-  const NmLayout L = nm_layout(M, N);
+  // another launch's QP size class: the M <= 15 class holds M + 1 lanes in one 16-lane row
+  if (M <= mz_lo || M > (kNmRows<MAXM> > 1 ? 15 : MAXM)) return;
+  const int G = kNmRows<MAXM> > 1 ? nm_groups(M, N) : 1;  // point buffers (uniform)
+  const NmLayout L = nm_layout(M, N, G);
   if ((long long)L.total * 8 <= lds_lo || (long long)L.total * 8 > lds_hi) return;  // another LDS tier
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
   double* sd = lds + L.dv;
   double* sxc = lds + L.xc;
-  double* sU = lds + L.u;
   double* sUo = lds + L.uo;
-  double* srw = lds + L.rw;
-  double* sR = lds + L.rr;
-  double* scv = lds + L.cv;
   double* snv = lds + L.nv;
   unsigned* sbits = reinterpret_cast<unsigned*>(lds + L.bits);
-  double* sxp = lds + L.xp;
-  double* ssx = lds + L.sx;
+  // point buffer g, and the current point's pieces (the factorisation the QP uses)
+  auto gbuf = [&](int g) __attribute__((always_inline)) -> double* { return lds + L.grp + g * L.gsz; };
+  double *sR, *scv, *sU, *sxp, *ssx;
+  auto setcur = [&](int g) __attribute__((always_inline)) {
+    double* b = gbuf(g);
+    sR = b + L.g_rr;
+    scv = b + L.g_cv;
+    sU = b + L.g_u;
+    sxp = b + L.g_xp;
+    ssx = b + L.g_sx;
+  };
+  setcur(0);
 
   const double* tab = sc.nm;  // [params][x0 3][u0 nu][lb nu][ub nu][xmin 3][xmax 3][sy ny][su nu]
   const VdV P = vdv_load(tab);
@@ -256,6 +288,14 @@ __global__ void __launch_bounds__(64, 1)
   const double* dl = deltav + c * ny;
   const double* lm = lambdav + c * nu;
   const double wu = fabs(lm[bn]) / sun;
+  // the lane's place in the multi-point pass: 16-lane row grp, lane gl of the row (the whole
+  // wave in the M <= 32 class); lanes gl < M carry tangent columns, gl = M the residual column
+  constexpr int R4 = kNmRows<MAXM>;
+  const int grp = R4 > 1 ? lane >> 4 : 0;
+  const int gl = R4 > 1 ? lane & 15 : lane;
+  const bool prow = gl < M;
+  const int pbn = prow ? gl / Nu : 0, pbl = prow ? gl - pbn * Nu : 0;
+  const double pwu = fabs(lm[pbn]) / tsu[pbn];
   int xc0 = sc.xc[0], xc1 = ny > 1 ? sc.xc[1] : 0;
   const double wy0 = fabs(dl[0]) / tsy[0], wy1 = ny > 1 ? fabs(dl[1]) / tsy[1] : 0.0;
   const double tol = o.feas_tol;
@@ -287,7 +327,13 @@ __global__ void __launch_bounds__(64, 1)
 
   // ---- one controller call (nlmpcmove restated): Gauss-Newton SQP from the warm start v
   // (this lane's increment), state x, last move ul[n], reference (r0, r1).  Returns v.
-  auto controller = [&](const double x[3], const double ul[2], double r0, double r1, double v)
+  // Speculation: a pass at a point this call may return also runs the next
+  // calls' first passes from it, assuming each of them returns its warm start at once.  hq[0] >= 0:
+  // point buffer hq[0] already holds this call's pass at v (speculated earlier), hq[1], hq[2] the
+  // following calls' (-1: none), hqf their costs.  t: this call's closed-loop step, nf: the
+  // future steps a speculation may reach (0..3).  sq / sqf: the chain for the returned point.
+  auto controller = [&](const double x[3], const double ul[2], double r0, double r1, double v, const int* hq,
+                        const double* hqf, int t, int nf, int* sq, double* sqf)
                         __attribute__((always_inline)) -> double {
     const double ulb = bn == 0 ? ul[0] : ul[1];
     // cost f(v') of increments v' by a tangent-free forward pass; xin: every predicted state
@@ -325,21 +371,60 @@ __global__ void __launch_bounds__(64, 1)
     // iteration's absolute-move step (aa_f, this lane's entry) and G (aa_g, increments)
     bool aa_hist = false;
     double aa_f = 0.0, aa_g = 0.0;
-    // the prediction at increments va with its forward tangents, streamed into the Givens QR of the
-    // least-squares Jacobian [rate rows; output rows] (R and c = Q'r -> LDS), the state rows of the
-    // linearised bounds (LDS) and the cost f(va); xin: every predicted state inside the hard bounds.
-    // Also the trial pass of a step: when the step is taken, its factorisation is the next
-    // iteration's, so an accepted trial costs one prediction instead of two.
-    auto full_pass = [&](double va, bool& xin) __attribute__((always_inline)) -> double {
-      // absolute moves of the iterate: U[n][l] = ul[n] + sum_{l' <= l} v[n][l']
+    // the prediction with forward tangents at the points whose increments the caller wrote into
+    // the point buffers, streamed into each point's Givens QR of the least-squares Jacobian
+    // [rate rows; output rows] (R and c = Q'r), its linearised state rows and its cost.  Point g
+    // runs on 16-lane row g (the whole wave in the M <= 32 class): the pass is bound by one wave's
+    // FP64 issue, so up to four points cost what one does.  A point with bit g of `spec` set is
+    // depth d_g = bits 2g..2g+1 of `dep` > 0 is the first point of the call d_g steps ahead from
+    // point g's increments, each call between returning its warm start at once: d_g plant steps
+    // with the first moves of the shifted increments, the increments shifted d_g moves (the closed
+    // loop's own update), that step's reference.  fg[g]: the cost f, xg[g]: every predicted state
+    // inside the hard bounds.
+    auto mpass = [&](unsigned dep, double* fg, bool* xg) __attribute__((always_inline)) {
+      lds_sync();  // the caller's increments
+      const bool gact = grp < G;  // rows without a buffer recompute point 0 and write nothing
+      double* gb = gbuf(gact ? grp : 0);
+      double* gv = gb + L.g_v;
+      double xs[3] = {x[0], x[1], x[2]};
+      double ug0 = ul[0], ug1 = ul[1], gr0 = r0, gr1 = r1;
+      double va = prow ? gv[gl] : 0.0;
+      if (dep) {
+        const int dg = gact ? (int)((dep >> (2 * grp)) & 3u) : 0;
+        int dm = 0;
+        for (int g = 0; g < 4; ++g) dm = max(dm, (int)((dep >> (2 * g)) & 3u));
+        for (int j = 1; j <= dm; ++j) {
+          // step j's applied moves: ul_(j-1) + the first moves of the increments shifted j - 1 times
+          const double m0 = j - 1 < Nu ? gv[j - 1] : 0.0;
+          const double m1 = nu > 1 && j - 1 < Nu ? gv[Nu + j - 1] : 0.0;
+          const double u1[2] = {ug0 + m0, nu > 1 ? ug1 + m1 : 0.0};
+          double xn[3] = {xs[0], xs[1], xs[2]};
+          vdv_rk4<false>(P, h, nsub, xn, u1, nullptr, nullptr);
+          if (j <= dg) {
+            xs[0] = xn[0];
+            xs[1] = xn[1];
+            xs[2] = xn[2];
+            ug0 = u1[0];
+            ug1 = u1[1];
+          }
+        }
+        if (dg > 0) {
+          gr0 = rr[t + dg];
+          gr1 = ny > 1 ? rr[nit + t + dg] : 0.0;
+          va = (prow && pbl + dg < Nu) ? gv[gl + dg] : 0.0;
+        }
+        lds_sync();
+        if (gact && prow) gv[gl] = va;
+      }
       lds_sync();
-      if (row) sxc[lane] = va;
-      lds_sync();
-      double cum = 0.0;
-      if (row) {
-        for (int j = lane - bl; j <= lane; ++j) cum += sxc[j];
-        sU[lane] = (bn == 0 ? ul[0] : ul[1]) + cum;
-        srw[lane] = wu * va;
+      // absolute moves of the point: U[n][l] = ul[n] + sum_{l' <= l} v[n][l']
+      double* gU = gb + L.g_u;
+      double* grw = gb + L.g_rw;
+      if (gact && prow) {
+        double cum = 0.0;
+        for (int j = gl - pbl; j <= gl; ++j) cum += gv[j];
+        gU[gl] = (pbn == 0 ? ug0 : ug1) + cum;
+        grw[gl] = pwu * va;
       }
       lds_sync();
       double rcol[MAXM];
@@ -347,30 +432,31 @@ __global__ void __launch_bounds__(64, 1)
       for (int k = 0; k < MAXM; ++k) {
         double e = 0.0;
         if (k < M) {
-          if (lane == k) e = wu;
-          else if (lane == M) e = srw[k];  // rate residual w_u v_k
+          if (gl == k) e = pwu;
+          else if (gl == M) e = grw[k];  // rate residual w_u v_k
         }
         rcol[k] = e;
       }
-      double xs[3] = {x[0], x[1], x[2]};
+      double* gxp = gb + L.g_xp;
+      double* gsx = gb + L.g_sx;
       double td[3] = {0.0, 0.0, 0.0};
-      double fo = 0.0;  // sum of squared output residuals (lane M)
+      double fo = 0.0;  // sum of squared output residuals (lane gl = M)
       bool inb = true;
       for (int i = 0; i < N; ++i) {
         const int li = i < Nu - 1 ? i : Nu - 1;
-        const double u[2] = {sU[li], nu > 1 ? sU[Nu + li] : 0.0};
+        const double u[2] = {gU[li], nu > 1 ? gU[Nu + li] : 0.0};
         double ud[2] = {0.0, 0.0};
-        if (row && bl <= li) ud[bn] = 1.0;
+        if (prow && pbl <= li) ud[pbn] = 1.0;
         vdv_rk4<true>(P, h, nsub, xs, u, td, ud);
         if (has_xb) {
-          if (row) {
-            ssx[(i * 3 + 0) * M + lane] = td[0];
-            ssx[(i * 3 + 1) * M + lane] = td[1];
-            ssx[(i * 3 + 2) * M + lane] = td[2];
-          } else if (lane == M) {
-            sxp[i * 3 + 0] = xs[0];
-            sxp[i * 3 + 1] = xs[1];
-            sxp[i * 3 + 2] = xs[2];
+          if (gact && prow) {
+            gsx[(i * 3 + 0) * M + gl] = td[0];
+            gsx[(i * 3 + 1) * M + gl] = td[1];
+            gsx[(i * 3 + 2) * M + gl] = td[2];
+          } else if (gact && gl == M) {
+            gxp[i * 3 + 0] = xs[0];
+            gxp[i * 3 + 1] = xs[1];
+            gxp[i * 3 + 2] = xs[2];
           }
           for (int s3 = 0; s3 < 3; ++s3) inb = inb && xs[s3] >= txmin[s3] && xs[s3] <= txmax[s3];
         }
@@ -379,14 +465,16 @@ __global__ void __launch_bounds__(64, 1)
           const double wy = j == 0 ? wy0 : wy1;
           if (!(wy > 0.0)) continue;
           double w = 0.0;
-          if (row) w = wy * sel3(td, xj);
-          else if (lane == M) w = wy * (sel3(xs, xj) - (j == 0 ? r0 : r1));
+          if (prow) w = wy * sel3(td, xj);
+          else if (gl == M) w = wy * (sel3(xs, xj) - (j == 0 ? gr0 : gr1));
           fo += w * w;
 #pragma unroll
           for (int k = 0; k < MAXM; ++k) {
             if (k < M) {
-              const double b = bcast(w, k);
-              const double a = bcast(rcol[k], k);
+              // the row's column-k entries: lane k of each 16-lane row (DPP row_newbcast), or of
+              // the wave
+              const double b = R4 > 1 ? row_bcast16(w, k) : bcast(w, k);
+              const double a = R4 > 1 ? row_bcast16(rcol[k], k) : bcast(rcol[k], k);
               // 1/rho by v_rsq_f64 and two Newton steps (a divide-free chain, as gpc_kernel's QR)
               const double xx = a * a + b * b;
               double ri = __builtin_amdgcn_rsq(xx);
@@ -402,29 +490,60 @@ __global__ void __launch_bounds__(64, 1)
           }
         }
       }
-      // R (upper, lane j holds column j) and c = Q'r (lane M) -> LDS
-      if (row || lane == M) {
+      // R (upper, lane j holds column j) and c = Q'r (lane M) -> the point's buffer
+      if (gact && (prow || gl == M)) {
+        double* gR = gb + L.g_rr;
+        double* gc = gb + L.g_cv;
 #pragma unroll
         for (int k = 0; k < MAXM; ++k)
           if (k < M) {
-            if (row) sR[k * M + lane] = rcol[k];
-            else scv[k] = rcol[k];
+            if (prow) gR[k * M + gl] = rcol[k];
+            else gc[k] = rcol[k];
           }
       }
-      xin = inb;
-      return 0.5 * (bcast(fo, M) + qsum<MAXM>(row ? (wu * va) * (wu * va) : 0.0));
+      const double rv2 = prow ? (pwu * va) * (pwu * va) : 0.0;
+      const double rs = R4 > 1 ? row_sum(rv2) : qsum<MAXM>(rv2);
+      for (int g = 0; g < G; ++g) {
+        fg[g] = 0.5 * (bcast(fo, 16 * g + M) + bcast(rs, 16 * g));
+        xg[g] = __builtin_amdgcn_readlane((int)inb, 16 * g) != 0;
+      }
     };
-    bool have = false;  // LDS holds the factorisation at v (an accepted trial pass)
-    double fcur = 0.0;
+    // point g's increments (lanes < M hold them) -> its buffer
+    auto put = [&](int g, double val) __attribute__((always_inline)) {
+      if (row) gbuf(g)[L.g_v + lane] = val;
+    };
+    // cur: buffer of the pass at v (-1: none yet); ch[0..2]: the buffers of the next calls'
+    // passes from v (-1: none), chf their costs
+    int cur = hq[0], ch[3] = {hq[1], hq[2], -1};
+    double fcur = hqf[0], chf[3] = {hqf[1], hqf[2], 0.0};
+    double fg[4] = {0.0, 0.0, 0.0, 0.0};
+    bool xg[4] = {true, true, true, true};
+    for (int k = 0; k < 3; ++k) {
+      sq[k] = -1;
+      sqf[k] = 0.0;
+    }
+    // one point's pass on every buffer: the point, then the next calls' first points (G = 4:
+    // three, G = 2: one), as far as the closed loop reaches
+    const int ndep = min(nf, G - 1);
+    const unsigned dchain = (ndep >= 1 ? 0x4u : 0u) | (ndep >= 2 ? 0x20u : 0u) | (ndep >= 3 ? 0xC0u : 0u);
+    auto chain_of_solo = [&]() __attribute__((always_inline)) {
+      for (int k = 0; k < 3; ++k) {
+        ch[k] = k < ndep ? k + 1 : -1;
+        chf[k] = k < ndep ? fg[k + 1] : 0.0;
+      }
+    };
     for (int it = 0; it < sc.sqp_max; ++it) {
       ++sqp_total;
       PSTAMP(PROF_NM_OTHER);
-      if (!have) {
-        bool xin_;
-        fcur = full_pass(v, xin_);
+      if (cur < 0) {
+        for (int g = 0; g < G; ++g) put(g, v);
+        mpass(dchain, fg, xg);
         PSTAMP(PROF_NM_FULL);
+        cur = 0;
+        fcur = fg[0];
+        chain_of_solo();
       }
-      have = false;
+      setcur(cur);
       const double f0 = fcur;
       lds_sync();
       // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
@@ -541,13 +660,20 @@ __global__ void __launch_bounds__(64, 1)
         }
       }
       PSTAMP(PROF_NM_QP);
-      // ---- convergence on the absolute-move change of the full step (oracle: max|d|/s_u)
+      // ---- convergence on the absolute-move change of the full step (oracle: max|d|/s_u); the
+      // iterate itself is returned (its pass, and the next call's first pass from it, are done)
       const double dpre = block_prefix<MAXM>(xm, bl, Nu, row, sxc);
       double chg = row ? fabs(dpre) / sun : 0.0;
       if (!isfinite(chg)) chg = INFINITY;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) chg = fmax(chg, __shfl_xor(chg, off, 64));
-      if (chg <= sc.sqp_tol) return v + (row ? xm : 0.0);
+      if (chg <= sc.sqp_tol) {
+        for (int k = 0; k < 3; ++k) {
+          sq[k] = ch[k];
+          sqf[k] = chf[k];
+        }
+        return v;
+      }
       if (!(chg < INFINITY)) {
         st |= MPCT_ST_NONFINITE_;
         return v;
@@ -563,7 +689,8 @@ __global__ void __launch_bounds__(64, 1)
       // absolute moves scaled by 1/s_u, candidate clip(G(v) - gamma (G(v) - G(v'))); taken when
       // it meets the Armijo decrease of the full step and respects the state bounds
       const double gv = v + (row ? xm : 0.0);
-      bool taken = false;
+      bool have_aa = false;
+      double vc = 0.0;
       if (aa_hist) {
         const double wdf = row ? (dpre - aa_f) / sun : 0.0;
         const double den = qsum<MAXM>(wdf * wdf);
@@ -573,39 +700,82 @@ __global__ void __launch_bounds__(64, 1)
           const double pc = block_prefix<MAXM>(vc0, bl, Nu, row, sxc);
           const double ucl = fmin(fmax(ulb + pc, lbn), ubn);
           const double upl = lane_prev<MAXM>(ucl);
-          const double vc = row ? (bl == 0 ? ucl - ulb : ucl - upl) : 0.0;
-          bool xin;
-          PSTAMP(PROF_NM_OTHER);
-          const double fc = full_pass(vc, xin);
-          PSTAMP(PROF_NM_AA);
-          if (xin && fc <= f0 + kLsC1 * dd) {
-            v = vc;
-            taken = true;
-            have = true;
-            fcur = fc;
-          }
+          vc = row ? (bl == 0 ? ucl - ulb : ucl - upl) : 0.0;
+          have_aa = true;
         }
       }
       aa_f = row ? dpre : 0.0;
       aa_g = gv;
       aa_hist = true;
-      if (taken) continue;
       // ---- Armijo backtracking on the cost along the step (oracle/nmpc_vdv.py controller):
       // halve alpha until f(v + alpha s) <= f0 + c1 alpha dd or the cost change is below its own
-      // rounding; the last alpha is taken regardless
+      // rounding; the last alpha is taken regardless.  The Anderson candidate and the full step
+      // (alpha = 1) share one pass when the point buffers allow (G > 1), with the next call's
+      // first pass from each (G = 4)
       double alpha = 1.0;
-      for (int ls = 0; ls < kLsMax; ++ls) {
+      int ls0 = 0;        // first Armijo step still to try
+      bool taken = false;
+      if (have_aa) {
+        PSTAMP(PROF_NM_OTHER);
+        const double va1 = v + (row ? alpha * xm : 0.0);
+        put(0, vc);
+        if (G > 1) put(1, va1);
+        if (G > 3) {
+          put(2, vc);
+          put(3, va1);
+        }
+        // G = 4: the Anderson candidate and the full step on rows 0, 1, the next call's first
+        // point from each on rows 2, 3
+        const bool sp4 = G > 3 && nf > 0;
+        mpass(sp4 ? 0x50u : 0u, fg, xg);
+        PSTAMP(PROF_NM_AA);
+        if (xg[0] && fg[0] <= f0 + kLsC1 * dd) {
+          v = vc;
+          cur = 0;
+          fcur = fg[0];
+          ch[0] = sp4 ? 2 : -1;
+          chf[0] = fg[2];
+          ch[1] = ch[2] = -1;
+          taken = true;
+        } else if (G > 1) {
+          const double f1 = fg[1];
+          if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
+            v = va1;
+            cur = 1;
+            fcur = f1;
+            ch[0] = sp4 ? 3 : -1;
+            chf[0] = fg[3];
+            ch[1] = ch[2] = -1;
+            taken = true;
+          } else {
+            alpha *= 0.5;
+            ls0 = 1;
+          }
+        }
+      }
+      if (taken) continue;
+      cur = -1;
+      ch[0] = ch[1] = ch[2] = -1;
+      for (int ls = ls0; ls < kLsMax; ++ls) {
         bool xin;
         // the full step's trial is a full pass (usually taken), shorter steps a tangent-free one
         const double va = v + (row ? alpha * xm : 0.0);
         PSTAMP(PROF_NM_OTHER);
-        const double f1 = ls == 0 ? full_pass(va, xin) : trial(va, xin);
-        if (ls == 0) PSTAMP(PROF_NM_LS0);
-        else PSTAMP(PROF_NM_TRIAL);
+        double f1;
+        if (ls == 0) {
+          for (int g = 0; g < G; ++g) put(g, va);
+          mpass(dchain, fg, xg);
+          f1 = fg[0];
+          PSTAMP(PROF_NM_LS0);
+        } else {
+          f1 = trial(va, xin);
+          PSTAMP(PROF_NM_TRIAL);
+        }
         if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
           if (ls == 0) {
-            have = true;
+            cur = 0;
             fcur = f1;
+            chain_of_solo();
           }
           break;
         }
@@ -624,7 +794,12 @@ __global__ void __launch_bounds__(64, 1)
   double vop = 0.0;
   double jnu = 0.0;
   if (o.open_loop) {
-    vop = controller(x0, u0, ny > 0 ? rr[nit - 1] : 0.0, ny > 1 ? rr[nit + nit - 1] : 0.0, 0.0);
+    const int hq0[3] = {-1, -1, -1};
+    const double hqf0[3] = {0.0, 0.0, 0.0};
+    int sq_[3];
+    double sqf_[3];
+    vop = controller(x0, u0, ny > 0 ? rr[nit - 1] : 0.0, ny > 1 ? rr[nit + nit - 1] : 0.0, 0.0, hq0, hqf0, 0, 0,
+                     sq_, sqf_);
     // absolute moves -> sU (held in LDS for the open-loop simulation)
     if (row) sxc[lane] = vop;
     lds_sync();
@@ -652,13 +827,23 @@ __global__ void __launch_bounds__(64, 1)
   double xo[3] = {x0[0], x0[1], x0[2]};
   double ul[2] = {u0[0], u0[1]};
   double v = 0.0;  // warm start: moves held at u0
+  // point buffers holding the next calls' first passes (speculated by earlier calls), their costs
+  int hq[3] = {-1, -1, -1};
+  double hqf[3] = {0.0, 0.0, 0.0};
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
   bool inb = true;
   const int ink0 = sc.ink0;
   for (int t = 0; t < nit; ++t) {
     if (t > 0) {
       const double r0 = rr[t], r1 = ny > 1 ? rr[nit + t] : 0.0;
-      v = controller(x, ul, r0, r1, v);
+      // this call also runs the first passes of up to three later calls (hq, hqf)
+      int sq[3];
+      double sqf[3];
+      v = controller(x, ul, r0, r1, v, hq, hqf, t, min(3, nit - 1 - t), sq, sqf);
+      for (int k = 0; k < 3; ++k) {
+        hq[k] = sq[k];
+        hqf[k] = sqf[k];
+      }
       // the first move U(:,t) = u(t-1) + v[n][0]
       if (row) sxc[lane] = v;
       lds_sync();
@@ -736,11 +921,12 @@ __global__ void __launch_bounds__(64, 1)
 
 namespace mpct {
 
-// LDS tiers (KB) of the class launches: M <= 16 class 12 workgroups per CU up to 13 KB, M <= 32
-// class 5 up to 32 KB, the rest above (finer tiers measured slower)
-constexpr long long kNmCap16Kb = 13, kNmCap32Kb = 32;
+// LDS tiers (KB) of the class launches.  One wave per SIMD (342 / 418 VGPRs), so at most four
+// workgroups per CU: the M <= 15 class sizes its point buffers to 40 KB (nm_groups), one tier;
+// the M <= 32 class 32 KB, the rest above (finer tiers measured slower)
+constexpr long long kNmCap16Kb = 40, kNmCap32Kb = 32;
 
-long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N).total * 8; }
+long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N, nm_groups(M, N)).total * 8; }
 
 // one launch per (QP size class MAXM 16 / 32) x (LDS tier), heaviest first, fanned over the
 // streams of launch_fan.h so the tiers overlap; a simulation runs in the launch of its class and
@@ -750,8 +936,11 @@ template <int MAXM>
 static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
                          const double* lambda, const double* r, const int* perm, const DevOpts& o,
                          const DevResult& out, FanScope& fs, int& nl, int mz_lo, bool& first, std::string* err) {
-  const int Mhi = std::min(sc.nu * sc.numax, MAXM);
-  const long long lds_max = nmpc_lds_bytes(Mhi, sc.n2max);
+  const int Mhi = std::min(sc.nu * sc.numax, kNmRows<MAXM> > 1 ? 15 : MAXM);
+  long long lds_max = 0;  // the class's largest simulation (the point buffers depend on M and N)
+  for (int m = mz_lo + 1; m <= Mhi; ++m)  // not monotone in N: the point buffers drop 4 -> 2 at 40 KB
+    for (int n = 1; n <= sc.n2max; ++n) lds_max = std::max(lds_max, nmpc_lds_bytes(m, n));
+  if (lds_max == 0) return 0;
   // LDS tiers (KB) of the class launches; the last one takes the rest up to lds_max
   static const long long c16[] = {kNmCap16Kb}, c32[] = {kNmCap32Kb};
   const long long* caps = MAXM <= 16 ? c16 : c32;
@@ -797,7 +986,7 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
   FanScope fs(fan, stream);  // forks after the sort: every class launch waits for the permutation
   int nl = 0, rc = 0;
   bool first = true;  // the first launch also writes the padding / bad-horizon statuses
-  if (Mmax > 16) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 16, first, err);
+  if (Mmax > 15) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 15, first, err);
   if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);
   fs.join();
   if (perm) order_mark_used(*wo, stream);  // after the join: every class launch has read it

@@ -71,6 +71,28 @@ __device__ __forceinline__ double row_sum(double v) {
   v += dppd<kMirror>(v);
   return v;
 }
+// lane k (0..15, a compile-time constant after unrolling) of every 16-lane row, broadcast over its
+// row: DPP row_newbcast (gfx950), no SGPR round trip; four rows give four independent broadcasts
+__device__ __forceinline__ double row_bcast16(double v, int k) {
+  switch (k & 15) {
+    case 0: return dppd<0x150>(v);
+    case 1: return dppd<0x151>(v);
+    case 2: return dppd<0x152>(v);
+    case 3: return dppd<0x153>(v);
+    case 4: return dppd<0x154>(v);
+    case 5: return dppd<0x155>(v);
+    case 6: return dppd<0x156>(v);
+    case 7: return dppd<0x157>(v);
+    case 8: return dppd<0x158>(v);
+    case 9: return dppd<0x159>(v);
+    case 10: return dppd<0x15A>(v);
+    case 11: return dppd<0x15B>(v);
+    case 12: return dppd<0x15C>(v);
+    case 13: return dppd<0x15D>(v);
+    case 14: return dppd<0x15E>(v);
+    default: return dppd<0x15F>(v);
+  }
+}
 __device__ __forceinline__ void row_argmin_step(double& v, int& id, double pv, int pi) {
   if (pv < v || (pv == v && pi < id)) {
     v = pv;

@@ -100,7 +100,7 @@ static int gi_qp(const double* Rinv, int M, int Nu, int nu, const double* bnd, c
       }
     }
     if (!(best < -tol)) break;
-    if (it >= maxit || q >= M) {
+    if (it >= maxit) { /* q == M is legal: beta = 0, the step is a dual one (a drop) */
       *st |= 1;
       break;
     }

@@ -291,8 +291,9 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None):
                     d, _, _ = qp_dual_dense(A, res, Aall, ball, qr=True)
         lo_b, hi_b = np.repeat(LB, Nu), np.repeat(UB, Nu)
         if np.max(np.abs(d) / su) <= SQP_TOL:
-            v = np.clip(v + d, lo_b, hi_b)
-            U = v.reshape(NU, Nu).T.copy()
+            # converged: the iterate itself is returned (not v + d, |d| <= SQP_TOL s_u), so the
+            # device can run the next call's first prediction from it alongside its last trial
+            # pass (nmpc_kernel.hip mpass)
             break
         # Armijo backtracking on the cost along the Gauss-Newton step: pure Gauss-Newton 2-cycles
         # on the large-residual steps of this reactor (e.g. after the setpoint change)
