@@ -106,21 +106,34 @@ __device__ __forceinline__ void row_argmin(double& v, int& id) {
   row_argmin_step(v, id, dppd<kMirror>(v), dppi<kMirror>(id));
 }
 
-__device__ __forceinline__ double wave_sum64(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-__device__ __forceinline__ void wave_argmin64(double& v, int& id) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double ov = __shfl_xor(v, off, 64);
-    int oid = __shfl_xor(id, off, 64);
-    if (ov < v || (ov == v && oid < id)) {
-      v = ov;
-      id = oid;
-    }
+// min of (v, id) with the partner half / row pair: v_permlane16/32_swap hand each lane its own and
+// its partner's value (in either order), so the lexicographic min of the pair is symmetric
+template <bool R32>
+__device__ __forceinline__ void pair_argmin(double& v, int& id) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  auto l = R32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false) : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  auto h = R32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false) : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  auto k = R32 ? __builtin_amdgcn_permlane32_swap(id, id, false, false) : __builtin_amdgcn_permlane16_swap(id, id, false, false);
+  double a = __hiloint2double(h[0], l[0]);
+  const double b = __hiloint2double(h[1], l[1]);
+  int ia = k[0];
+  const int ib = k[1];
+  if (b < a || (b == a && ib < ia)) {
+    a = b;
+    ia = ib;
   }
+  v = a;
+  id = ia;
+}
+
+// reductions over the whole wave: DPP within the 16-lane rows, then the v_permlane16/32_swap
+// exchanges between rows (gfx950) -- no LDS round trip.  A __shfl_xor butterfly costs six
+// ds_bpermute round trips per value; the band kernel's M > 15 classes and the NMPC's M > 15
+// class run several of these per QP iteration
+__device__ __forceinline__ void wave_argmin64(double& v, int& id) {
+  row_argmin(v, id);
+  pair_argmin<false>(v, id);
+  pair_argmin<true>(v, id);
 }
 
 // sum over the four 16-lane rows (lanes l, l+16, l+32, l+48), result in every row:
@@ -136,6 +149,8 @@ __device__ __forceinline__ double row4_sum(double v) {
   auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
   return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
 }
+
+__device__ __forceinline__ double wave_sum64(double v) { return row4_sum(row_sum(v)); }
 
 // reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
 template <int MAXM>
