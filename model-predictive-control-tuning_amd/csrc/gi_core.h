@@ -126,10 +126,16 @@ template <int MAXM>
 __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
   const int lane = qp_lane();
   double ck = lane < S.q ? c : 0.0, rk = 0.0;
+  // R_A(lane, w) is loaded one step ahead, off the chain of broadcasts (LDS latency was exposed at
+  // every step: config 3's q ~ 40 active sets)
+  const bool in = lane < M;
+  double a = in && S.q > 0 ? sRA[lane * M + S.q - 1] : 0.0;
   for (int w = S.q - 1; w >= 0; --w) {
+    const double an = in && w > 0 ? sRA[lane * M + w - 1] : 0.0;
     const double rw = bcast(ck * S.rdg, w);
     if (lane == w) rk = rw;
-    if (lane < w) ck -= sRA[lane * M + w] * rw;
+    if (lane < w) ck -= a * rw;
+    a = an;
   }
   return rk;
 }

@@ -133,6 +133,10 @@ __global__ void __launch_bounds__(64, 1)
   const int M = nu * Nu, Mz = M + 1;
   const int P = my * N2;
   int st = 0;
+#ifdef MPCT_PROFILE
+  unsigned long long pacc[PROF_N] = {};
+  unsigned long long pprev = __builtin_amdgcn_s_memtime();
+#endif
 
   auto write_nan = [&](int status) __attribute__((always_inline)) {
     if (lane < my) {
@@ -359,6 +363,16 @@ __global__ void __launch_bounds__(64, 1)
       const double* sp = sstep + (i * nu + n) * tls + (k + 1);
       const double* xp = sxc + n * Nu;
       int l = 0;
+      // four taps per trip, their loads issued together; the accumulation order (even taps into
+      // a0, odd into a1) is the two-tap loop's
+      for (; l + 3 <= lmax; l += 4) {
+        const double s0 = sp[-l], s1 = sp[-l - 1], s2 = sp[-l - 2], s3 = sp[-l - 3];
+        const double x0 = xp[l], x1 = xp[l + 1], x2 = xp[l + 2], x3 = xp[l + 3];
+        a0 += s0 * x0;
+        a1 += s1 * x1;
+        a0 += s2 * x2;
+        a1 += s3 * x3;
+      }
       for (; l + 1 <= lmax; l += 2) {
         a0 += sp[-l] * xp[l];
         a1 += sp[-l - 1] * xp[l + 1];
@@ -406,6 +420,14 @@ __global__ void __launch_bounds__(64, 1)
       const double* jc = sJT + lane * Mz;
       double d1 = 0.0;
       int r = 0;
+      for (; r + 3 < Mz; r += 4) {  // four terms' loads together, the two-term loop's order
+        const double j0 = jc[r], j1 = jc[r + 1], j2 = jc[r + 2], j3 = jc[r + 3];
+        const double n0 = snv[r], n1 = snv[r + 1], n2 = snv[r + 2], n3 = snv[r + 3];
+        dk += j0 * n0;
+        d1 += j1 * n1;
+        dk += j2 * n2;
+        d1 += j3 * n3;
+      }
       for (; r + 1 < Mz; r += 2) {
         dk += jc[r] * snv[r];
         d1 += jc[r + 1] * snv[r + 1];
@@ -420,6 +442,7 @@ __global__ void __launch_bounds__(64, 1)
   // one toolbox QP at the window F, reference r (lane i < my holds r_i), MV u_prev in LDS;
   // result in sxc (moves 0..M-1, eps at M)
   auto solve = [&](const double* F, double r_i) __attribute__((always_inline)) {
+    PSTAMP(PROF_PLANT);
     // ---- unconstrained minimiser x_u = -R^-1 R^-T g, g = G'Q(F - r)  (g = 0 in band mode)
     double xu = 0.0;
     if (any_q) {
@@ -475,6 +498,7 @@ __global__ void __launch_bounds__(64, 1)
       lds_sync();
       // key = slack / |n o D| over the rows violated beyond tol; best = the winner's raw slack
       double key = INFINITY;
+      double kraw = INFINITY;  // the raw slack of this lane's best row (handed to every lane below)
       bid = 0x7fffffff;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -490,6 +514,7 @@ __global__ void __launch_bounds__(64, 1)
           const double kk = s[k] * ibk;
           if (kk < key) {
             key = kk;
+            kraw = s[k];
             bid = 4 * lane + k;
           }
         }
@@ -508,6 +533,7 @@ __global__ void __launch_bounds__(64, 1)
             const double kk = s_up * (double)srn[q];
             if (kk < key) {
               key = kk;
+              kraw = s_up;
               bid = base + q;
             }
           }
@@ -522,21 +548,17 @@ __global__ void __launch_bounds__(64, 1)
             const double kk = s_lo * (double)srn[q];
             if (kk < key) {
               key = kk;
+              kraw = s_lo;
               bid = base + q;
             }
           }
         }
       }
       wave_argmin64(key, bid);
-      if (key == INFINITY) {
-        best = INFINITY;
-      } else if (bid < base) {  // the winner's raw slack: a box row of lane bid >> 2
-        const int k = bid & 3;
-        const double sv = k == 0 ? s[0] : (k == 1 ? s[1] : (k == 2 ? s[2] : s[3]));
-        best = bcast(sv, bid >> 2);
-      } else {
-        best = out_slack(F, bid - base, eps);
-      }
+      // the winner's raw slack, from the lane that scanned it: box row 4 m + kind on lane m, output
+      // row q = 2 g + side on lane g mod 64 (the scan's own value: no second prediction of that row)
+      if (key == INFINITY) best = INFINITY;
+      else best = bcast(kraw, bid < base ? (bid >> 2) : (((bid - base) >> 1) & (kWave - 1)));
     };
     int it = 0;   // all factorisation work (GI steps + rebuild re-adds + re-centring drops): qp_iters
     int git = 0;  // GI add/drop steps only: the iteration cap guards against cycling, not rebuilds
@@ -586,11 +608,18 @@ __global__ void __launch_bounds__(64, 1)
         }
         double wv = 0.0;
         x = row ? xu : 0.0;
-        for (int v = 0; v < q; ++v) {  // R_A'w = c, x = x_u + J(:,0:q) w
+        // R_A'w = c, x = x_u + J(:,0:q) w; step v's R_A and J entries are loaded one step ahead,
+        // off the chain of broadcasts
+        double ra = lane < Mz ? sRA[lane] : 0.0, jv = row ? sJT[lane] : 0.0;
+        for (int v = 0; v < q; ++v) {
+          const int vn = v + 1 < q ? v + 1 : v;
+          const double ran = lane < Mz ? sRA[vn * Mz + lane] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
           const double w = bcast(cc * gis.rdg, v);
           if (lane == v) wv = w;
-          if (lane > v && lane < q) cc -= sRA[v * Mz + lane] * w;
-          if (row) x += sJT[v * Mz + lane] * w;
+          if (lane > v && lane < q) cc -= ra * w;
+          if (row) x += jv * w;
+          ra = ran;
+          jv = jvn;
         }
         const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv);
         if (lane < q) gis.uw = lam;
@@ -624,6 +653,7 @@ __global__ void __launch_bounds__(64, 1)
         gis.jinit = false;
       } else {
         xm = eqp_from_xu(s, false);
+        PSTAMP(PROF_QWARM);
       }
     }
     int npolish = 0;
@@ -631,6 +661,7 @@ __global__ void __launch_bounds__(64, 1)
       double best, s[4];
       int bid;
       most_violated(xm, best, bid, s, false);
+      PSTAMP(PROF_QCHECK);
       if (!(best < -tol_acc)) {
         // optimal up to the incremental updates: after a long QP re-solve the final active set
         // exactly from x_u (fresh J) and re-check every row before accepting
@@ -640,6 +671,7 @@ __global__ void __launch_bounds__(64, 1)
           ++dbg_pol;
 #endif
           xm = recentre(true);
+          PSTAMP(PROF_QWARM);
           continue;
         }
         break;
@@ -651,6 +683,7 @@ __global__ void __launch_bounds__(64, 1)
       }
       if (gis.q > 0 && gis.nrot >= MPCT_XP_DRIFT_K * Mz) {  // J has drifted: rebuild it and re-centre x
         xm = recentre(true);
+        PSTAMP(PROF_QWARM);
         continue;
       }
       if (!gis.jinit) load_j();
@@ -666,6 +699,7 @@ __global__ void __launch_bounds__(64, 1)
         const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
         lds_sync();
         const double zm = gi_z(sJT, sd, gis.q, Mz, row);
+        PSTAMP(PROF_QD);
         const double rk = gi_backsub<MAXM>(gis, sRA, Mz, dk);
         double t1 = INFINITY;
         int kdrop = 0x7fffffff;
@@ -674,6 +708,7 @@ __global__ void __launch_bounds__(64, 1)
           kdrop = lane;
         }
         qargmin<MAXM>(t1, kdrop);
+        PSTAMP(PROF_QR);
         const double t2 = (beta > 1e-20 * dn2) ? -qp_div(sp, beta) : INFINITY;
         if (t1 == INFINITY && t2 == INFINITY) {
           st |= MPCT_ST_QP_INFEAS_;
@@ -688,9 +723,11 @@ __global__ void __launch_bounds__(64, 1)
         sp += t * beta;
         if (full) {
           gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark);
+          PSTAMP(PROF_QADD);
           break;
         }
         gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark);
+        PSTAMP(PROF_QDROP);
         if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;
           break;
@@ -703,6 +740,7 @@ __global__ void __launch_bounds__(64, 1)
       }
     }
     if (row) sxc[lane] = xm;
+    PSTAMP(PROF_QP);
     lds_sync();
 #ifdef MPCT_DEBUG_BAND
     dbg_git = git;
@@ -741,6 +779,7 @@ __global__ void __launch_bounds__(64, 1)
     }
   }
 
+  PSTAMP(PROF_PROLOGUE);
   // ------------------------------------------------------------------ closed loop
   double j1 = 0.0, j21 = 0.0, j22 = 0.0;
   const int ncopy = o.open_loop ? 2 : 1;
@@ -905,6 +944,11 @@ __global__ void __launch_bounds__(64, 1)
     yr_t = yr_n;
   }
 
+#ifdef MPCT_PROFILE
+  PSTAMP(PROF_PLANT);
+  if (lane == 0 && out.prof)
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+#endif
   // ------------------------------------------------------------------ results
   if (lane < my) {
     if (!isfinite(j1)) st |= MPCT_ST_NONFINITE_;

@@ -1,13 +1,10 @@
 set -o pipefail
-O=gpurun_out/r04o; mkdir -p $O
-timeout -k 10 240 python3 -u tools/config3_ab.py > $O/config3_ab.jsonl 2> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
+O=gpurun_out/r04u; mkdir -p $O
+L=$PWD/model-predictive-control-tuning_amd/csrc
+for v in _base _kraw ""; do
+  MPCT_LIB=$L/libmpct$v.so timeout -k 10 240 python3 -u tools/config3_ab.py >> $O/config3_ab.jsonl 2>> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
+done
 cat $O/config3_ab.jsonl
-timeout -k 10 180 python3 -u tools/nmpc_latency.py > $O/nmpc_latency.txt 2>&1 || { tail -20 $O/nmpc_latency.txt; exit 1; }
-grep "C=1" $O/nmpc_latency.txt
-timeout -k 10 180 python3 -u tools/bench_config5.py > $O/bench_config5.txt 2>&1 || { tail -20 $O/bench_config5.txt; exit 1; }
-tail -1 $O/bench_config5.txt
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
-tail -2 $O/pytest_gpu.log
-timeout -k 10 300 python3 -u tools/diag/gam_calls.py 60 > $O/gam_calls.txt 2>&1 || { tail -20 $O/gam_calls.txt; exit 1; }
-tail -4 $O/gam_calls.txt
+MPCT_LIB=$L/libmpct_bprof.so timeout -k 10 120 python3 -u tools/diag/band_step_debug.py 8015 $O/slow.npz > $O/band_prof_8015.txt 2>&1 || { tail -20 $O/band_prof_8015.txt; exit 1; }
+grep -v amdgpu $O/band_prof_8015.txt | head -15
 echo diag done
