@@ -395,21 +395,21 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
       }
       lds_sync();
       // equality-constrained solve on the retained set, dropping negative multipliers:
-      // w = R_A^-T c = B'c, x = x_u + J(:,0:q) w, lambda = R_A^-1 w = B w
+      // w = R_A^-T c = B'c, x = x_u + J(:,0:q) w, lambda = R_A^-1 w = B w.
+      // c = b_A - N_A'x_u: lane w < q gathers the slack at x_u of its constraint ww = 4 m + kind
+      // from QP row m (ds_bpermute; no LDS buffer), once: a drop shifts c with the ids
+      double c;
+      {
+        const int src = (S.ww >= 0 ? S.ww >> 2 : 0) + 16 * q16_b();
+        const double g0 = __shfl(s[0], src, kWave), g1 = __shfl(s[1], src, kWave);
+        const double g2 = __shfl(s[2], src, kWave), g3 = __shfl(s[3], src, kWave);
+        c = i < S.q ? -sel4v_v(g0, g1, g2, g3, S.ww & 3) : 0.0;
+      }
       for (;;) {
         const int q = S.q;
         if (q == 0) {
           xm = xu;
           break;
-        }
-        // c = b_A - N_A'x_u: lane w < q gathers the slack at x_u of its constraint ww = 4 m + kind
-        // from QP row m (ds_bpermute; no LDS buffer)
-        double c;
-        {
-          const int src = (S.ww >= 0 ? S.ww >> 2 : 0) + 16 * q16_b();
-          const double g0 = __shfl(s[0], src, kWave), g1 = __shfl(s[1], src, kWave);
-          const double g2 = __shfl(s[2], src, kWave), g3 = __shfl(s[3], src, kWave);
-          c = i < q ? -sel4v_v(g0, g1, g2, g3, S.ww & 3) : 0.0;
         }
         d4v Bl, w;
         b_row4(F.sB, Bl);
@@ -431,6 +431,11 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         qargmin<16>(lmin, kd, 0);
         if (!(lmin < 0.0)) break;
         gi16_drop(S, F, sRA, M, kd, mark);
+        {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
+          const double cn = lane_next<16>(c);
+          if (i >= kd && i < q - 1) c = cn;
+          else if (i == q - 1) c = 0.0;
+        }
         ++it;
       }
       if (!row) xm = 0.0;

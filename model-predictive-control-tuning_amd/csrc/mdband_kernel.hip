@@ -34,9 +34,12 @@
 #endif
 // J is rebuilt and x re-centred after MPCT_XP_DRIFT_K x Mz rotations.  16 against 4 with the
 // normalised constraint choice: config-3 grid 1.67 against 1.70 s, slowest simulation 189 against
-// 198 ms, F beyond 1e-6 of the C port 2.04 against 2.19 % (profiles/r04f_config3_ab.jsonl)
+// 198 ms, F beyond 1e-6 of the C port 2.04 against 2.19 % (profiles/r04f_config3_ab.jsonl); with
+// the relative termination test 64 against 16: 1.54-1.55 against 1.57 s, 154-155 against 159 ms,
+// F 1.34 against 1.40 %; 128, 256 and never rebuilding measured the same as 64 (the final polish
+// re-solves long QPs anyway; profiles/r04w_*, r04x_config3_rebuild_interval_sweep.jsonl)
 #ifndef MPCT_XP_DRIFT_K
-#define MPCT_XP_DRIFT_K 16
+#define MPCT_XP_DRIFT_K 64
 #endif
 // the QP stops when no constraint's normalised slack is below -kRelTol max(1, |normalised bound|):
 // the oracle's own test (toolbox_band.py qp_dual_dense, oracle/cband.c dual_solve).  Against the

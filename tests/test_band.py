@@ -15,10 +15,10 @@ TRAJ_RTOL = 1e-7      # free-run trajectories, relative to the trajectory's peak
 REPLAY_RTOL = 1e-6    # per-step first moves at the device's own states, relative to max |du|
 COST_RTOL = 1e-6      # BASELINE tolerance on the costs
 # config-3 full-grid ranking against the C port (test_band_config3_grid_costs_against_c_port):
-# bounds just above the values measured on the GPU (profiles/r04l_config3_reltol_ab.jsonl,
-# the oracle's relative QP termination test: 2,994 candidates displaced, largest displacement
-# 1,361, 2,727 discordant pairs of which 2,603 beyond the 1e-6 bar)
-CONFIG3_RANK_BOUNDS = dict(displaced=3100, max_disp=1400, discordant=2850, significant=2700)
+# bounds just above the values measured on the GPU (profiles/r04x_config3_rebuild_interval_sweep.jsonl,
+# the oracle's relative QP termination test, rebuild interval 64 Mz: 2,754 candidates displaced,
+# largest displacement 1,361, 2,498 discordant pairs of which 2,385 beyond the 1e-6 bar)
+CONFIG3_RANK_BOUNDS = dict(displaced=2850, max_disp=1400, discordant=2600, significant=2500)
 
 
 def _trel(a, b):
@@ -445,9 +445,9 @@ def test_band_config3_grid_costs_against_c_port(gpu):
     oracle/cband.c):
     * every simulation succeeds, and the top-64 ranking under SHELL7_W (Shell7x5.m:202, what the
       tuner consumes) is identical;
-    * at most 1.5 % of the candidates' Pareto-weighted costs F = J1 @ SHELL7_W differ by more than
-      1e-6 relative (measured 1.39 %, profiles/r04l_config3_reltol_ab.jsonl), and at most 8.5 % of
-      the stratified sample's per-output J1 (measured 7.85 %);
+    * at most 1.45 % of the candidates' Pareto-weighted costs F = J1 @ SHELL7_W differ by more than
+      1e-6 relative (measured 1.34 %, profiles/r04x_config3_rebuild_interval_sweep.jsonl), and at
+      most 8.5 % of the stratified sample's per-output J1 (measured 7.80 %);
     * the full-grid ranking under F (rank_stats): candidates displaced, the largest displacement,
       discordant pairs and discordant pairs the 1e-6 bar separates are bounded just above their
       measured values (DESIGN §3), so a regression that widens the divergence fails;
@@ -479,7 +479,7 @@ def test_band_config3_grid_costs_against_c_port(gpu):
     rs = rank_stats(F, d["F_full"])
     print("config3: F beyond 1e-6: %.4f of the grid (median %.1e); J1 beyond 1e-6: %.4f of the sample; "
           "ranking %s" % (np.mean(relF > COST_RTOL), np.median(relF), np.mean(relJ > COST_RTOL), rs))
-    assert np.mean(relF > COST_RTOL) <= 0.015
+    assert np.mean(relF > COST_RTOL) <= 0.0145
     assert np.mean(relJ > COST_RTOL) <= 0.085
     for k, bound in CONFIG3_RANK_BOUNDS.items():
         assert rs[k] <= bound, (k, rs[k], bound)
