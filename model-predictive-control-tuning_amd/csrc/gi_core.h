@@ -112,6 +112,15 @@ __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int 
   double z0 = 0.0, z1 = 0.0;
   if (row) {
     int k = q;
+    for (; k + 3 < M; k += 4) {  // four terms' loads together, the two-term loop's order
+      const double j0 = sJT[k * M + lane], j1 = sJT[(k + 1) * M + lane];
+      const double j2 = sJT[(k + 2) * M + lane], j3 = sJT[(k + 3) * M + lane];
+      const double d0 = sd[k], d1 = sd[k + 1], d2 = sd[k + 2], d3 = sd[k + 3];
+      z0 += j0 * d0;
+      z1 += j1 * d1;
+      z0 += j2 * d2;
+      z1 += j3 * d3;
+    }
     for (; k + 1 < M; k += 2) {
       z0 += sJT[k * M + lane] * sd[k];
       z1 += sJT[(k + 1) * M + lane] * sd[k + 1];
@@ -156,7 +165,17 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     const double jq = sJT[q * M + lane];
     const double f = (zm - alpha * jq) * two_vtv;
     sJT[q * M + lane] = jq - f * vq;
-    for (int k = q + 1; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
+    int k = q + 1;
+    for (; k + 3 < M; k += 4) {  // independent columns: four loads in flight
+      const double j0 = sJT[k * M + lane], j1 = sJT[(k + 1) * M + lane];
+      const double j2 = sJT[(k + 2) * M + lane], j3 = sJT[(k + 3) * M + lane];
+      const double d0 = sd[k], d1 = sd[k + 1], d2 = sd[k + 2], d3 = sd[k + 3];
+      sJT[k * M + lane] = j0 - f * d0;
+      sJT[(k + 1) * M + lane] = j1 - f * d1;
+      sJT[(k + 2) * M + lane] = j2 - f * d2;
+      sJT[(k + 3) * M + lane] = j3 - f * d3;
+    }
+    for (; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
   if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
   const double ia = qp_rcp(alpha);
