@@ -284,7 +284,8 @@ def vns2_batched(par: TuningPar, batch_evaluate, fv: float, max_batch: int = 512
 
 # --------------------------------------------------------------------------------------------
 def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_change: float = 0.5,
-                    max_iter: int = 400, ftol: float = 1e-3, speculate: bool = False):
+                    max_iter: int = 400, ftol: float = 1e-3, speculate: bool = False,
+                    max_fun_evals: int | None = None, memo: dict | None = None):
     """GAM step of MPC_TFob.m:61-67: fgoalattain(@GAM_fun, x0, goal=0.001, weight=w, lb=1e-5,
     EqualityGoalCount = numel(w)) -- restated as the goal-attainment problem
         min gamma  s.t.  |J1_i(x) - goal| <= w_i * gamma,  x >= lb1
@@ -303,13 +304,22 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
     closed loops waits for its slowest one (91 s against 88 s unbatched, same endpoint).  Scoring
     the backtracking steps ahead as well needs SLSQP's trial points bit for bit, which its caller
     cannot reproduce; points matched to 13 digits moved the search to another endpoint.  Off by
-    default.  Points are cached by their exact value."""
+    default.  Points are cached by their exact value.
+    max_fun_evals: fgoalattain's MaxFunctionEvaluations, which MPCTuning.m:88-91 leaves at its
+    default of 100 * numel(x0).  MATLAB counts every call of the objective, line-search trials and
+    forward-difference points alike; here every distinct point the search asks for.  The search
+    stops after the iteration that reaches the budget and returns that iterate (MATLAB's exitflag
+    0).  memo: a point cache that outlives the call (mpc_tfob keeps one per (max N, max Nu), so a
+    GAM round that repeats an earlier one from the same start costs no engine call); the values
+    and the evaluation-order bookkeeping are the same as without it."""
     from scipy.optimize import minimize
 
     my, ny = par.my, par.ny
     n = my + ny
     w = np.asarray(par.w, dtype=float)
-    cache = {}
+    if max_fun_evals is None:
+        max_fun_evals = 100 * n
+    cache = memo if memo is not None else {}
     nb = [0]
     last = [None]
     last_eval = [None]
@@ -373,9 +383,25 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
          "jac": lambda z: np.hstack([jac_F(z[:-1])[1], w[:, None]])},
     ]
     bounds = [(lb, None) for lb in par.lb1] + [(None, None)]
-    res = minimize(lambda z: z[-1], z0, jac=lambda z: np.eye(n + 1)[-1], method="SLSQP",
-                   constraints=cons, bounds=bounds, options={"maxiter": max_iter, "ftol": ftol})
-    x = np.maximum(res.x[:-1], par.lb1)
+
+    class _Budget(Exception):
+        pass
+
+    iterate = [z0]
+
+    def budget(zk):
+        iterate[0] = np.array(zk, dtype=float)
+        if len(asked) >= max_fun_evals:
+            raise _Budget
+
+    try:
+        res = minimize(lambda z: z[-1], z0, jac=lambda z: np.eye(n + 1)[-1], method="SLSQP",
+                       constraints=cons, bounds=bounds, callback=budget,
+                       options={"maxiter": max_iter, "ftol": ftol})
+        zf = res.x
+    except _Budget:
+        zf = iterate[0]
+    x = np.maximum(zf[:-1], par.lb1)
     final_eval = last_eval[0]   # the search's own last evaluation, before the report below
     Fx = F(x)
     attain = float(np.max(np.abs(Fx - goal) / w))
@@ -391,7 +417,8 @@ def gam_fgoalattain(par: TuningPar, batch_j1, goal: float = 1e-3, diff_min_chang
 
 # --------------------------------------------------------------------------------------------
 def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, gam_max_iter: int = 400,
-             fgam_from: str = "last_eval", stale=None, gam_speculate: bool = False):
+             fgam_from: str = "last_eval", stale=None, gam_speculate: bool = False,
+             gam_max_fun_evals: int | None = None):
     """MPC_TFob.m:28-143: alternate GAM (weights) and VNS (horizons) until a GAM round does not
     improve.  Quirks kept: Fgam = round(sum(F), 2) where F is the global GAM_fun.m:114 set on its
     LAST call (MPC_TFob.m:104), i.e. the J1 of fgoalattain's last evaluated point, not of the
@@ -404,8 +431,11 @@ def mpc_tfob(par: TuningPar, batch_j1, batch_vns, fv: float = 1e30, log=None, ga
     hi = 0
     delta = lam = None
     Fvns = fv
+    memo = {}
     while True:
-        x, attain, Fx, ncalls, Flast = gam_fgoalattain(par, batch_j1, max_iter=gam_max_iter, speculate=gam_speculate)
+        x, attain, Fx, ncalls, Flast = gam_fgoalattain(
+            par, batch_j1, max_iter=gam_max_iter, speculate=gam_speculate, max_fun_evals=gam_max_fun_evals,
+            memo=memo.setdefault((int(np.max(par.N)), int(np.max(par.Nu))), {}))
         x = x.copy()
         x[:my][par.ov_zero] = 0.0
         par.x0 = x
@@ -561,14 +591,16 @@ def stale_rows_for(yref, inK: int = 10) -> StaleRows:
 def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None, q0=None, w0=None,
                device: int = -1, log=None, save_path: str | None = None, scale: dict | None = None,
                gam_max_iter: int = 400, lineal: bool = True, mdv=None, fgam_from: str = "last_eval",
-               stale_rows: bool = True, gam_speculate: bool = False):
+               stale_rows: bool = True, gam_speculate: bool = False, gam_max_fun_evals: int | None = None):
     """MPCTuning.m:93-381 on an already scaled scenario (mpct.scenarios builds Pze = L*Pz*R, the
     scaled bounds, L*Xsp and L*Yref from the committed L, R -- MPCTuning.m:154-189).  Returns
     (N, Nu, delta, lambda, Fob = [Fvns, Fgam]) and optionally writes Tuning_Parameters.
     lineal = False: a nonlinear (NMPC) scenario (MPCTuning.m:202-250): VNS simulates the driver's
     setpoint one output at a time instead of unit steps (VNS2.m:67-71,148-155).
     fgam_from / stale_rows: the MPC_TFob.m:104 and VNS2.m:151-163 quirks (mpc_tfob, StaleRows);
-    "returned" / False give the round-2 behaviour (Fgam at the returned point, failed -> NaN)."""
+    "returned" / False give the round-2 behaviour (Fgam at the returned point, failed -> NaN).
+    gam_max_fun_evals: fgoalattain's MaxFunctionEvaluations (None: its default 100 * (my + ny),
+    which MPCTuning.m:88-91 keeps; gam_fgoalattain)."""
     par = TuningPar(my=my, ny=ny, nbp=nbp, nbc=nbc, dmin=dmin, w=w, q0=q0, w0=w0, nit=sc.nit)
     if sc.n2_max < 2 ** par.nbp - 1 or sc.nu_max < 2 ** par.nbc - 1:
         raise ValueError("scenario horizons (n2_max=%d, nu_max=%d) must cover the bit ranges "
@@ -586,7 +618,7 @@ def mpc_tuning(sc, r, my: int, ny: int, w, nbp: int = 7, nbc: int = 4, dmin=None
         batch_vns = batch_vns.rows
     N, Nu, lam, delta, Fvns, Fgam, _ = mpc_tfob(par, batch_j1, batch_vns, fv=1e30, log=log,
                                                   gam_max_iter=gam_max_iter, fgam_from=fgam_from, stale=stale,
-                                                  gam_speculate=gam_speculate)
+                                                  gam_speculate=gam_speculate, gam_max_fun_evals=gam_max_fun_evals)
     if save_path:
         save_tuning_parameters(save_path, N, Nu, delta, lam, scale=scale)
     return N, Nu, delta, lam, np.array([Fvns, Fgam])

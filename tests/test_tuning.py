@@ -116,6 +116,42 @@ def test_gam_goal_attainment_synthetic():
     assert nb >= 2
 
 
+def test_gam_function_evaluation_budget_and_memo():
+    """fgoalattain's MaxFunctionEvaluations (default 100 * numel(x0); MPCTuning.m:88-91 does not
+    set it) counts every evaluated point, forward differences included: the search stops after the
+    iteration that reaches it.  A memo shared by two identical GAM rounds (mpc_tfob) makes the
+    second one free and identical."""
+    a = np.array([1.0, 3.0, 0.5])
+    pts = []
+
+    def batch_j1(X):
+        X = np.atleast_2d(X)
+        pts.extend(map(tuple, X))
+        J0 = np.abs(X[:, 0] - a[0]) ** 1.5 + 0.1 * X[:, 2] ** 2 + np.sin(7 * X[:, 1]) ** 2
+        J1 = (X[:, 1] - a[1]) ** 2 + 0.1 * X[:, 2] ** 2 + 1e-3
+        return np.stack([J0, J1], axis=1)
+
+    par = TuningPar(my=2, ny=1, w=np.array([0.5, 0.5]))
+    par.x0 = np.array([2.0, 2.0, 2.0])
+    x_free, *_ = gam_fgoalattain(par, batch_j1, max_iter=400, max_fun_evals=10 ** 6)
+    n_free = len(set(pts))
+    pts.clear()
+    x, att, Fx, nb, last = gam_fgoalattain(par, batch_j1, max_iter=400, max_fun_evals=12)
+    n_cap = len(set(pts) - {tuple(x)})
+    assert n_free > 20 and 12 <= n_cap <= 12 + 2 * (par.my + par.ny + 1)
+    assert np.all(x >= par.lb1) and att == pytest.approx(np.max(np.abs(Fx - 1e-3) / par.w))
+    # default budget: 100 * numel(x0)
+    pts.clear()
+    gam_fgoalattain(par, batch_j1, max_iter=400)
+    assert len(set(pts)) <= 300 + 2 * (par.my + par.ny + 1) + 1
+    memo = {}
+    r1 = gam_fgoalattain(par, batch_j1, max_iter=30, memo=memo)
+    r2 = gam_fgoalattain(par, batch_j1, max_iter=30, memo=memo)
+    assert r1[3] > 0 and r2[3] == 0
+    for u, v in zip(r1[:3] + r1[4:], r2[:3] + r2[4:]):
+        np.testing.assert_array_equal(u, v)
+
+
 def test_tuning_parameters_roundtrip(tmp_path):
     from scipy.io import loadmat
 

@@ -40,14 +40,17 @@ def score_point(sc, r, N, Nu, delta, lam, w, mdv=None, vns_refs=None):
 def run(name, sc, r, my, ny, w, nbp, nbc, dmin, q0, w0, scale=None, mdv=None, lineal=True, out=None,
         gam_max_iter=400):
     """Environment knobs for A/B runs: MPCT_GAM_SPECULATE=1 (each trial point scored with its
-    difference points), MPCT_FGAM_FROM=returned, MPCT_STALE_ROWS=0 (the round-2 quirk handling)."""
+    difference points), MPCT_FGAM_FROM=returned, MPCT_STALE_ROWS=0 (the round-2 quirk handling),
+    MPCT_GAM_MAX_FEVALS=n (fgoalattain's MaxFunctionEvaluations; default 100 * numel(x0))."""
     from mpct.tuning import mpc_tuning
 
     out = out or os.path.join(ROOT, "gpurun_out", "%s_Tuning.mat" % name)
     t0 = time.time()
     heartbeat(t0)
-    log("%s: MPCTuning(nbp=%d, nbc=%d, w=%s, q0=%s, w0=%s, GAM max %d iterations) speculate=%s fgam=%s stale=%s"
-        % (name, nbp, nbc, list(np.round(w, 6)), list(q0), list(w0), gam_max_iter,
+    fev = os.environ.get("MPCT_GAM_MAX_FEVALS")
+    log("%s: MPCTuning(nbp=%d, nbc=%d, w=%s, q0=%s, w0=%s, GAM max %d iterations, max %s evaluations) speculate=%s "
+        "fgam=%s stale=%s"
+        % (name, nbp, nbc, list(np.round(w, 6)), list(q0), list(w0), gam_max_iter, fev or "100*numel(x0)",
            os.environ.get("MPCT_GAM_SPECULATE", "0"), os.environ.get("MPCT_FGAM_FROM", "last_eval"),
            os.environ.get("MPCT_STALE_ROWS", "1")))
     N, Nu, delta, lam, Fob = mpc_tuning(sc, r, my=my, ny=ny, w=w, nbp=nbp, nbc=nbc, dmin=dmin, q0=q0, w0=w0,
@@ -55,7 +58,8 @@ def run(name, sc, r, my, ny, w, nbp, nbc, dmin, q0, w0, scale=None, mdv=None, li
                                         lineal=lineal, mdv=mdv,
                                         gam_speculate=os.environ.get("MPCT_GAM_SPECULATE", "0") == "1",
                                         fgam_from=os.environ.get("MPCT_FGAM_FROM", "last_eval"),
-                                        stale_rows=os.environ.get("MPCT_STALE_ROWS", "1") != "0")
+                                        stale_rows=os.environ.get("MPCT_STALE_ROWS", "1") != "0",
+                                        gam_max_fun_evals=int(fev) if fev else None)
     dt = time.time() - t0
     log("N=%s Nu=%s delta=%s lambda=%s Fob=%s  (%.1f s)" % (N, Nu, delta, lam, Fob, dt))
     return N, Nu, delta, lam, Fob, dt
