@@ -130,17 +130,34 @@ __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int 
   return z0 + z1;
 }
 
+// R_A's place in LDS.  RAFull: row-major, row stride M (M x M).  RAPacked: column-major upper
+// Hessenberg, column j holding rows 0..j+1 (the drop's shifted columns carry one subdiagonal entry
+// until its Givens rotation clears it), M (M + 3) / 2 doubles: the band kernel's R_A at Mz = 46 is
+// 8.6 KB smaller, which moves its heaviest simulations to a denser LDS tier.  Same arithmetic in
+// both layouts; every index either layout forms stays inside its array.
+struct RAFull {
+  int M;
+  static constexpr bool packed = false;
+  __device__ __forceinline__ int operator()(int i, int j) const { return i * M + j; }
+};
+struct RAPacked {
+  static constexpr bool packed = true;
+  __device__ __forceinline__ int operator()(int i, int j) const { return ((j * (j + 3)) >> 1) + i; }
+};
+__host__ __device__ constexpr int ra_packed_size(int M) { return (M * (M + 3)) / 2; }
+
 // r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
-template <int MAXM>
-__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
+template <int MAXM, class RAL>
+__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c,
+                                             const RAL& ra) {
   const int lane = qp_lane();
   double ck = lane < S.q ? c : 0.0, rk = 0.0;
   // R_A(lane, w) is loaded one step ahead, off the chain of broadcasts (LDS latency was exposed at
   // every step: config 3's q ~ 40 active sets)
   const bool in = lane < M;
-  double a = in && S.q > 0 ? sRA[lane * M + S.q - 1] : 0.0;
+  double a = in && S.q > 0 ? sRA[ra(lane, S.q - 1)] : 0.0;
   for (int w = S.q - 1; w >= 0; --w) {
-    const double an = in && w > 0 ? sRA[lane * M + w - 1] : 0.0;
+    const double an = in && w > 0 ? sRA[ra(lane, w - 1)] : 0.0;
     const double rw = bcast(ck * S.rdg, w);
     if (lane == w) rk = rw;
     if (lane < w) ck -= a * rw;
@@ -148,12 +165,16 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
   }
   return rk;
 }
+template <int MAXM>
+__device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const double* sRA, int M, double c) {
+  return gi_backsub<MAXM>(S, sRA, M, c, RAFull{M});
+}
 
 // append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
-template <int MAXM, class Mark>
+template <int MAXM, class Mark, class RAL>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
-                                       const Mark& mark) {
+                                       const Mark& mark, const RAL& ra) {
   const int lane = qp_lane();
   const int q = S.q;
   const double dq = bcast(dk, q);
@@ -177,10 +198,10 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     }
     for (; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
-  if (lane < q) sRA[lane * M + q] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  if (lane < q) sRA[ra(lane, q)] = dk;  // new column q of R_A = [d(0:q-1); alpha]
   const double ia = qp_rcp(alpha);
   if (lane == q) {
-    sRA[q * M + q] = alpha;
+    sRA[ra(q, q)] = alpha;
     S.rdg = ia;
     S.uw = upm;
     S.ww = p;
@@ -190,17 +211,25 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
   S.nrot += 1;
   lds_sync();
 }
+template <int MAXM, class Mark>
+__device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
+                                       int p, double dk, double beta, double zm, double upm, bool row,
+                                       const Mark& mark) {
+  gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, mark, RAFull{M});
+}
 
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
-template <int MAXM, class Mark>
+template <int MAXM, class Mark, class RAL>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
-                                        const Mark& mark) {
+                                        const Mark& mark, const RAL& ra) {
   const int lane = qp_lane();
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);
-  if (lane < q) {  // remove column kd (lanes = rows)
-    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
+  if (lane < q) {  // remove column kd (lanes = rows; rows below w + 1 of the new column w are
+                   // never read, and the packed column w holds no more)
+    for (int w = kd; w < q - 1; ++w)
+      if (!RAL::packed || lane <= w + 1) sRA[ra(lane, w)] = sRA[ra(lane, w + 1)];
   }
   {
     const double un = lane_next<MAXM>(S.uw);
@@ -214,15 +243,15 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
   // R_A is upper Hessenberg in columns kd..q-2: Givens on rows (jj, jj+1), lanes = columns
   for (int jj = kd; jj < q - 1; ++jj) {
     {
-      const double a = sRA[jj * M + jj], b = sRA[(jj + 1) * M + jj];
+      const double a = sRA[ra(jj, jj)], b = sRA[ra(jj + 1, jj)];
       const double rr = a * a + b * b;
       if (rr != 0.0) {
         const double ri = rsq_nr(rr);
         const double cs = a * ri, sn = b * ri;
         if (lane >= jj && lane < q - 1) {
-          const double r0 = sRA[jj * M + lane], r1 = sRA[(jj + 1) * M + lane];
-          sRA[jj * M + lane] = cs * r0 + sn * r1;
-          sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
+          const double r0 = sRA[ra(jj, lane)], r1 = sRA[ra(jj + 1, lane)];
+          sRA[ra(jj, lane)] = cs * r0 + sn * r1;
+          sRA[ra(jj + 1, lane)] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
         }
         if (lane < M) {
           const double j0v = sJT[jj * M + lane], j1v = sJT[(jj + 1) * M + lane];
@@ -239,9 +268,14 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
     S.uw = 0.0;
     S.ww = -1;
   }
-  if (lane < qn) S.rdg = qp_rcp(sRA[lane * M + lane]);
+  if (lane < qn) S.rdg = qp_rcp(sRA[ra(lane, lane)]);
   S.q = qn;
   lds_sync();
+}
+template <int MAXM, class Mark>
+__device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
+                                        const Mark& mark) {
+  gi_drop<MAXM>(S, sJT, sRA, M, kd, mark, RAFull{M});
 }
 
 

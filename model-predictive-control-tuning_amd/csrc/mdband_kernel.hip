@@ -56,7 +56,14 @@ namespace mpct {
 struct BandLayout {
   int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, rn, plb, pla,
       mzb, mza, total;
+  int yh, ur, ts;  // entry output ring, input ring (powers of two) and tail stride of this scenario
 };
+
+__host__ __device__ inline int pow2_at_least(int n) {
+  int r = 1;
+  while (r < n) r <<= 1;
+  return r;
+}
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
@@ -76,22 +83,29 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.ri = take(full_ri ? Mz * Mz : Mz);
   L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
-  L.ra = take(Mz * Mz);  // R_A
+  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked)
   L.dv = take(Mz);       // d = J'n
   L.nv = take(Mz);       // staged normal n_p
   L.xc = take(Mz);       // QP iterate
   L.gv = take(full_ri ? Mz : 0);  // linear term / triangular-solve scratch (tracking weights only)
   L.sl = take(4 * Mz);   // box slacks at the unconstrained minimiser
   L.ob = take(4 * my);   // y_min, y_max, V_min s_y, V_max s_y
-  L.fr = take(2 * my * N2);                // free-response window, double-buffered by t parity
+  L.fr = take(my * N2);                    // free-response window, shifted in place every step
   L.bits = take((2 * my * N2 + 63) / 64);  // active output rows (32-bit words)
   L.du = take(nu);                         // du(t-1)
   L.uprev = take(nu);
   L.ucum = take(ncopy == 2 ? M : 0);  // open-loop Uopt only
+  // the rings hold what the recursions read back: an entry's last pl_maxa outputs; the inputs of
+  // the longest numerator (delay included) and the window tails' t - 1 (Shell 7x5: 2 and 16
+  // instead of the general kernel's 8 and 32, 6.6 KB less LDS per simulation)
+  const int nbmax = sc.pl_maxb > sc.mz_maxb ? sc.pl_maxb : sc.mz_maxb;
+  L.yh = pow2_at_least(sc.pl_maxa);
+  L.ur = pow2_at_least(nbmax > 2 ? nbmax : 2);
+  L.ts = sc.mz_maxa > 2 ? sc.mz_maxa - 1 : 1;
   L.ye = take(ncopy * ne);
-  L.yeh = take(ncopy * ne * kYeHist);
-  L.uring = take(ncopy * nin * kURing);
-  L.tail = take(ne * kYeHist);  // model entry tails of the window
+  L.yeh = take(ncopy * ne * L.yh);
+  L.uring = take(ncopy * nin * L.ur);
+  L.tail = take(ne * L.ts);  // model entry tails of the window (mz_na - 1 entries each)
   L.sext = take(ne);            // model entry window extensions
   L.rn = take(my * N2);         // output rows' inverse norms: 2 floats (upper, lower) per row
   L.plb = take(ne * sc.pl_maxbc);  // compact: taps from the first nonzero one
@@ -177,6 +191,7 @@ __global__ void __launch_bounds__(64, 1)
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
+  const RAPacked rap{};
   double* sd = lds + L.dv;
   double* snv = lds + L.nv;
   double* sxc = lds + L.xc;
@@ -192,6 +207,7 @@ __global__ void __launch_bounds__(64, 1)
   double* syeh = lds + L.yeh;
   double* sur = lds + L.uring;
   double* stail = lds + L.tail;
+  const int umask = L.ur - 1, ymask = L.yh - 1;
   double* sext = lds + L.sext;
   double* splb = lds + L.plb;
   double* spla = lds + L.pla;
@@ -587,7 +603,7 @@ __global__ void __launch_bounds__(64, 1)
           lds_sync();
           const double zm = gi_z(sJT, sd, v, Mz, row);
           const double uk = gis.uw;
-          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark);
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap);
           if (lane == v) gis.uw = uk;
           ++it;
         }
@@ -613,10 +629,10 @@ __global__ void __launch_bounds__(64, 1)
         x = row ? xu : 0.0;
         // R_A'w = c, x = x_u + J(:,0:q) w; step v's R_A and J entries are loaded one step ahead,
         // off the chain of broadcasts
-        double ra = lane < Mz ? sRA[lane] : 0.0, jv = row ? sJT[lane] : 0.0;
+        double ra = lane < Mz ? sRA[rap(0, lane)] : 0.0, jv = row ? sJT[lane] : 0.0;
         for (int v = 0; v < q; ++v) {
           const int vn = v + 1 < q ? v + 1 : v;
-          const double ran = lane < Mz ? sRA[vn * Mz + lane] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
+          const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
           const double w = bcast(cc * gis.rdg, v);
           if (lane == v) wv = w;
           if (lane > v && lane < q) cc -= ra * w;
@@ -624,13 +640,13 @@ __global__ void __launch_bounds__(64, 1)
           ra = ran;
           jv = jvn;
         }
-        const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv);
+        const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv, rap);
         if (lane < q) gis.uw = lam;
         double lmin = lane < q ? lam : INFINITY;
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark);
+        gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap);
         ++it;
       }
       return row ? x : 0.0;
@@ -703,7 +719,7 @@ __global__ void __launch_bounds__(64, 1)
         lds_sync();
         const double zm = gi_z(sJT, sd, gis.q, Mz, row);
         PSTAMP(PROF_QD);
-        const double rk = gi_backsub<MAXM>(gis, sRA, Mz, dk);
+        const double rk = gi_backsub<MAXM>(gis, sRA, Mz, dk, rap);
         double t1 = INFINITY;
         int kdrop = 0x7fffffff;
         if (lane < gis.q && rk > 0.0) {
@@ -725,11 +741,11 @@ __global__ void __launch_bounds__(64, 1)
         upm += t;
         sp += t * beta;
         if (full) {
-          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark);
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap);
           PSTAMP(PROF_QADD);
           break;
         }
-        gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark);
+        gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap);
         PSTAMP(PROF_QDROP);
         if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;
@@ -769,6 +785,8 @@ __global__ void __launch_bounds__(64, 1)
       for (int j = lane - rcn.l; j <= lane; ++j) s += sxc[j];
       sucum[lane] = s;  // Uopt row l of MV n (held after Nu-1)
     }
+    // the closed loop's first step shifts a zero window (the open-loop one is done with)
+    for (int g = lane; g < P; g += kWave) sfr[g] = 0.0;
     lds_sync();
     if (lane < nu) {
       // VNS2.m:183-191: Xnu = |uopt(:,1)| ./ |diff(uopt)|, inf/NaN -> 0, Jnu = sum Xnu^2
@@ -800,11 +818,11 @@ __global__ void __launch_bounds__(64, 1)
     // inputs known at t: MDs v(t) (both copies); the open-loop copy's MVs uopt(t)
     for (int e = lane; e < ncopy * nd; e += kWave) {
       const int cpy = e / nd, j = e - cpy * nd;
-      sur[(cpy * nin + nu + j) * kURing + (t & (kURing - 1))] = vvk[j * nit + t];
+      sur[(cpy * nin + nu + j) * L.ur + (t & umask)] = vvk[j * nit + t];
     }
     if (o.open_loop && lane < nu) {
       const int l = t < Nu - 1 ? t : Nu - 1;
-      sur[(nin + lane) * kURing + (t & (kURing - 1))] = sucum[lane * Nu + l];
+      sur[(nin + lane) * L.ur + (t & umask)] = sucum[lane * Nu + l];
     }
     lds_sync();
     // plant entries y_e(t) (copy 0 closed loop, copy 1 open loop driven by uopt)
@@ -812,14 +830,14 @@ __global__ void __launch_bounds__(64, 1)
       const int cpy = e / ne, ee = e - cpy * ne, j = ee % nin;
       const double* eb = splb + ee * sc.pl_maxbc - sc.pl_off[ee];  // tap l at eb[l], l >= off
       const double* ea = spla + ee * sc.pl_maxa;
-      const double* eur = sur + (cpy * nin + j) * kURing;
-      double* eyh = syeh + e * kYeHist;
+      const double* eur = sur + (cpy * nin + j) * L.ur;
+      double* eyh = syeh + e * L.yh;
       const int nb = sc.pl_nb[ee], na = sc.pl_na[ee], off = sc.pl_off[ee];
       double a0 = 0.0, a1 = 0.0;
-      for (int l = off; l < nb; ++l) a0 += eb[l] * eur[(t - l) & (kURing - 1)];
-      for (int l = 1; l < na; ++l) a1 -= ea[l] * eyh[(t - l) & (kYeHist - 1)];
+      for (int l = off; l < nb; ++l) a0 += eb[l] * eur[(t - l) & umask];
+      for (int l = 1; l < na; ++l) a1 -= ea[l] * eyh[(t - l) & ymask];
       const double acc = a0 + a1;
-      eyh[t & (kYeHist - 1)] = acc;
+      eyh[t & ymask] = acc;
       sye[e] = acc;
     }
     lds_sync();
@@ -847,8 +865,8 @@ __global__ void __launch_bounds__(64, 1)
       const int i = e / nin, j = e - i * nin;
       const double* mb = smzb + e * sc.mz_maxbc - sc.mz_off[e];  // tap l at mb[l], l >= off
       const double* ma = smza + e * sc.mz_maxa;
-      const double* eur = sur + j * kURing;
-      double* tl = stail + e * kYeHist;
+      const double* eur = sur + j * L.ur;
+      double* tl = stail + e * L.ts;
       const int nb = sc.mz_nb[e], na = sc.mz_na[e] - 1, off = sc.mz_off[e];
       if (j < nu) {
         const double dlt = sdu[j];
@@ -858,8 +876,8 @@ __global__ void __launch_bounds__(64, 1)
             if (N2 - l >= 0) tl[l] += sp[N2 - l] * dlt;
         }
       } else {
-        const double vt = eur[t & (kURing - 1)];
-        const double dlt = vt - (t > 0 ? eur[(t - 1) & (kURing - 1)] : 0.0);
+        const double vt = eur[t & umask];
+        const double dlt = vt - (t > 0 ? eur[(t - 1) & umask] : 0.0);
         if (dlt != 0.0) {
           const double* sp = sc.step_md + (i * nd + (j - nu)) * tlen;
           for (int l = 0; l < na; ++l)
@@ -870,7 +888,7 @@ __global__ void __launch_bounds__(64, 1)
       double a0 = 0.0, a1 = 0.0;
       for (int l = off; l < nb; ++l) {
         const int tau = min(t + N2 - l, tcap);
-        if (tau >= 0) a0 += mb[l] * eur[tau & (kURing - 1)];
+        if (tau >= 0) a0 += mb[l] * eur[tau & umask];
       }
       for (int l = 1; l <= na; ++l) a1 -= ma[l] * tl[l - 1];
       const double ext = a0 + a1;
@@ -879,12 +897,15 @@ __global__ void __launch_bounds__(64, 1)
       sext[e] = ext;
     }
     lds_sync();
-    const double* Fp = sfr + ((t + 1) & 1) * P;
-    double* Fc = sfr + (t & 1) * P;
+    // F(t) = shifted F(t-1) + the step's increments, in place: entry g reads g + 1 of the same
+    // output block before any lane stores g + 1 (one wave; the loads of a trip issue before its
+    // stores, and the clobber keeps the next trip's store of g + 64 behind this trip's load of it)
+    const double* Fp = sfr;
+    double* Fc = sfr;
     bool any_dv = false;
     for (int m = 0; m < nd; ++m) {
-      const double* vr = sur + (nu + m) * kURing;
-      any_dv = any_dv || (vr[t & (kURing - 1)] != (t > 0 ? vr[(t - 1) & (kURing - 1)] : 0.0));
+      const double* vr = sur + (nu + m) * L.ur;
+      any_dv = any_dv || (vr[t & umask] != (t > 0 ? vr[(t - 1) & umask] : 0.0));
     }
     for (int g = lane; g < P; g += kWave) {
       const int i = g / N2, k = g - i * N2;
@@ -894,8 +915,8 @@ __global__ void __launch_bounds__(64, 1)
         for (int n = 0; n < nu; ++n) f += sstep[(i * nu + n) * tls + k + 2] * sdu[n];
         if (any_dv) {
           for (int m = 0; m < nd; ++m) {
-            const double* vr = sur + (nu + m) * kURing;
-            const double dv = vr[t & (kURing - 1)] - (t > 0 ? vr[(t - 1) & (kURing - 1)] : 0.0);
+            const double* vr = sur + (nu + m) * L.ur;
+            const double dv = vr[t & umask] - (t > 0 ? vr[(t - 1) & umask] : 0.0);
             f += sc.step_md[(i * nd + m) * tlen + k + 1] * dv;
           }
         }
@@ -904,6 +925,7 @@ __global__ void __launch_bounds__(64, 1)
         for (int j = 0; j < nin; ++j) f += sext[i * nin + j];
       }
       Fc[g] = f;
+      asm volatile("" ::: "memory");
     }
     lds_sync();
 #ifdef MPCT_DEBUG_BAND
@@ -932,7 +954,7 @@ __global__ void __launch_bounds__(64, 1)
       const double du = sxc[n * Nu];
       const double un = suprev[n] + du;
       sdu[n] = du;
-      sur[n * kURing + (t & (kURing - 1))] = un;
+      sur[n * L.ur + (t & umask)] = un;
       if (o.want_traj) {
         if (out.u) out.u[(sim * nu + n) * nit + t] = un;
         if (o.open_loop && out.uopt) {
