@@ -67,11 +67,13 @@ __host__ __device__ inline int pow2_at_least(int n) {
 
 // LDS layout of one simulation; [fr, plb) holds the windows, the histories and the active-row
 // bitmap (zeroed at start)
-// LDS tiers of the class launches: 6/5/4/3/2/1 workgroups per CU (the last must be 160;
-// tools/ab3.sh: 4 tiers 3.09 s, these 2.88 s).  The QP reads the MV step table from global memory
-// (L1/L2-resident, shared by every simulation) instead of an LDS copy: 21.5 KB less LDS at
-// N2 = 127, 3.14 -> 3.09 s
-constexpr long long kBandCapsKb[] = {26, 32, 40, 53, 80, 160};
+// LDS tiers of the class launches: 8/6/5/4/3/2/1 workgroups per CU (the last must be 160;
+// tools/ab3.sh: 4 tiers 3.09 s, 6 tiers 2.88 s; after the round-4 LDS diet the 20 KB tier of
+// 8 per CU, the 216-VGPR kernel's limit, took the grid 1.03-1.05 -> 0.98 s, and a 7-per-CU
+// 22 KB tier or dropping the 26 or 32 KB tier were slower: profiles/r04zg_*, r04zh_*).  The QP
+// reads the MV step table from global memory (L1/L2-resident, shared by every simulation)
+// instead of an LDS copy: 21.5 KB less LDS at N2 = 127, 3.14 -> 3.09 s
+constexpr long long kBandCapsKb[] = {20, 26, 32, 40, 53, 80, 160};
 
 // full_ri: R^-1 is a full triangle (some OV weight > 0); in band mode R is diagonal and only its
 // inverse diagonal is kept.  ncopy: 2 with the open-loop prediction (a second plant copy), else 1

@@ -1,13 +1,13 @@
 set -o pipefail
-O=gpurun_out/r04zf; mkdir -p $O
+O=gpurun_out/r04zh; mkdir -p $O
 L=$PWD/model-predictive-control-tuning_amd/csrc
-for v in _base _fr ""; do
+for v in _c8 _c8b _c8c ""; do
   MPCT_LIB=$L/libmpct$v.so timeout -k 10 240 python3 -u tools/config3_ab.py >> $O/config3_ab.jsonl 2>> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
 done
 python3 -c "
 import json
 for l in open('$O/config3_ab.jsonl'):
     d=json.loads(l); print(d['lib'], round(d['grid_s'],3), round(d['slowest']['alone_ms'],1), d['F_beyond_1e-6'], d['rank'], d['status_nonzero'])"
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
-tail -3 $O/pytest_gpu.log
+true
+true
 echo diag done
