@@ -142,7 +142,10 @@ struct RAFull {
 };
 struct RAPacked {
   static constexpr bool packed = true;
-  __device__ __forceinline__ int operator()(int i, int j) const { return ((j * (j + 3)) >> 1) + i; }
+  // 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate): j <= 64
+  __device__ __forceinline__ int operator()(int i, int j) const {
+    return (int)(__umul24((unsigned)j, (unsigned)(j + 3)) >> 1) + i;
+  }
 };
 __host__ __device__ constexpr int ra_packed_size(int M) { return (M * (M + 3)) / 2; }
 

@@ -1,7 +1,7 @@
 set -o pipefail
-O=gpurun_out/r04zh; mkdir -p $O
+O=gpurun_out/r04zi; mkdir -p $O
 L=$PWD/model-predictive-control-tuning_amd/csrc
-for v in _c8 _c8b _c8c ""; do
+for v in _head "" _head ""; do
   MPCT_LIB=$L/libmpct$v.so timeout -k 10 240 python3 -u tools/config3_ab.py >> $O/config3_ab.jsonl 2>> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
 done
 python3 -c "
