@@ -37,10 +37,11 @@ def band_work_estimate(N2, Nu, lam, nu=3):
     return N2 ** 0.769 * M1 ** 2.067 * 10.0 ** (-0.0988 * lg)
 
 
-def shard_indices_keyed(work, world: int, rank: int) -> np.ndarray:
+def shard_indices_keyed(work, world: int, rank: int, heavy_first: bool = False) -> np.ndarray:
     """Work-keyed split: candidates sorted by descending estimated work, dealt to the ranks in snake
     order (0..W-1, W-1..0, ...), so every rank gets one candidate of every work level and the heavy
-    tail is spread evenly; each rank's candidates in ascending index order.  Pads like
+    tail is spread evenly; each rank's candidates in ascending index order, or with heavy_first in
+    descending estimated work (the band kernel dispatches in input order).  Pads like
     shard_indices (indices >= C are sentinels, dealt last)."""
     C = len(work)
     per = -(-C // world)
@@ -49,7 +50,8 @@ def shard_indices_keyed(work, world: int, rank: int) -> np.ndarray:
     pos = np.arange(per * world)
     rnd, j = pos // world, pos % world
     owner = np.where(rnd % 2 == 0, j, world - 1 - j)
-    return np.sort(order[owner == rank])
+    mine = order[owner == rank]
+    return mine if heavy_first else np.sort(mine)
 
 
 def pad_shard(N2, Nu, delta, lam, idx):

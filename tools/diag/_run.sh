@@ -1,13 +1,7 @@
 set -o pipefail
-O=gpurun_out/r04zi; mkdir -p $O
-L=$PWD/model-predictive-control-tuning_amd/csrc
-for v in _head "" _head ""; do
-  MPCT_LIB=$L/libmpct$v.so timeout -k 10 240 python3 -u tools/config3_ab.py >> $O/config3_ab.jsonl 2>> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
-done
+O=gpurun_out/r04zk; mkdir -p $O
+timeout -k 10 600 python3 -u tools/shard_balance.py --only shell7x5 --out $O/shard_balance.json > $O/shard_balance.log 2>&1 || { tail -20 $O/shard_balance.log; exit 1; }
 python3 -c "
-import json
-for l in open('$O/config3_ab.jsonl'):
-    d=json.loads(l); print(d['lib'], round(d['grid_s'],3), round(d['slowest']['alone_ms'],1), d['F_beyond_1e-6'], d['rank'], d['status_nonzero'])"
-true
-true
+import json; d=json.load(open('$O/shard_balance.json'))
+for k,v in d['shell7x5'].items(): print(k, [round(x) for x in v['shard_ms']], round(max(v['shard_ms'])), round(v['max_over_mean'],3))"
 echo diag done

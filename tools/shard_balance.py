@@ -1,7 +1,7 @@
 """Per-shard time of the 8-rank splits on one GPU: for config 3 (the 65,536
 Shell 7x5 grid, cell-ordered) and config 4 (10,000 WoodBerry DTC candidates x 32 draws), each of
 the 8 shards of the contiguous (round 2), strided (mpct.dist.shard_indices) and, for config 3,
-work-keyed (mpct.dist.shard_indices_keyed) splits is scored alone on cuda:0 and timed with HIP
+work-keyed (mpct.dist.shard_indices_keyed, candidates in index order or heaviest first) splits is scored alone on cuda:0 and timed with HIP
 events (median of 3); max/mean shard time predicts the 8-GPU efficiency loss from imbalance.
 Usage: python tools/shard_balance.py [--out FILE]"""
 import argparse
@@ -57,15 +57,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--only", default=None, help="shell7x5 or dtc-mc")
     a = ap.parse_args()
     W = a.world
     rep = {}
     for name in ("shell7x5", "dtc-mc"):
+        if a.only and name != a.only:
+            continue
         sc, cand, refs, v, nref = workload(name)
         C = len(cand[0])
         per = -(-C // W)
         res = {}
-        splits = ("contiguous", "strided", "keyed") if name == "shell7x5" else ("contiguous", "strided")
+        splits = ("contiguous", "strided", "keyed", "keyed_heavy_first") if name == "shell7x5" else ("contiguous", "strided")
         for split in splits:
             times = []
             for rk in range(W):
@@ -74,7 +77,8 @@ def main():
                 elif split == "strided":
                     idx = shard_indices(C, W, rk)
                 else:
-                    idx = shard_indices_keyed(band_work_estimate(cand[0], cand[1], cand[3]), W, rk)
+                    idx = shard_indices_keyed(band_work_estimate(cand[0], cand[1], cand[3]), W, rk,
+                                              heavy_first=split == "keyed_heavy_first")
                 times.append(time_shard(sc, cand, refs, v, nref, idx))
                 print(name, split, rk, "%.1f ms" % times[-1], flush=True)
             res[split] = dict(shard_ms=times, max_over_mean=max(times) / float(np.mean(times)))
