@@ -1,7 +1,13 @@
 set -o pipefail
-O=gpurun_out/r04zk; mkdir -p $O
-timeout -k 10 600 python3 -u tools/shard_balance.py --only shell7x5 --out $O/shard_balance.json > $O/shard_balance.log 2>&1 || { tail -20 $O/shard_balance.log; exit 1; }
+O=gpurun_out/r04zl; mkdir -p $O
+L=$PWD/model-predictive-control-tuning_amd/csrc
+for v in _head "" _head ""; do
+  MPCT_LIB=$L/libmpct$v.so timeout -k 10 240 python3 -u tools/config3_ab.py >> $O/config3_ab.jsonl 2>> $O/config3_ab.err || { tail -20 $O/config3_ab.err; exit 1; }
+done
 python3 -c "
-import json; d=json.load(open('$O/shard_balance.json'))
-for k,v in d['shell7x5'].items(): print(k, [round(x) for x in v['shard_ms']], round(max(v['shard_ms'])), round(v['max_over_mean'],3))"
+import json
+for l in open('$O/config3_ab.jsonl'):
+    d=json.loads(l); print(d['lib'], round(d['grid_s'],3), round(d['slowest']['alone_ms'],1), d['F_beyond_1e-6'], d['rank'], d['status_nonzero'])"
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_band.py > $O/pytest_band.log 2>&1 || { tail -30 $O/pytest_band.log; exit 1; }
+tail -2 $O/pytest_band.log
 echo diag done
