@@ -82,13 +82,21 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   double* sQ = sW + my * Mp;    // q_i
   double* sS = sQ + my;         // the step table [my][nu][tlen]
   double* sD = sS + my * nu * tlen;  // jump vectors of one pass [64][my]
-  int* sN1 = reinterpret_cast<int*>(sD + kWave * my);
+  double* sBn = sD + kWave * my;     // b_n per MV (read up front, off the jump passes' chain)
+  double* sLw = sBn + nu;            // the move weight of each MV (H's diagonal)
+  int* sN1 = reinterpret_cast<int*>(sLw + nu);
   for (int e = lane; e < my * nu * tlen; e += kWave) sS[e] = sc.step[e];
   if (lane < my) {
     const double di = fabs(delta[c * my + lane]);
     const double sqi = sc.wsq ? di : sqrt(di);
     sQ[lane] = sqi * sqi;
     sN1[lane] = sc.n1[lane];
+  }
+  if (lane < nu) {
+    sBn[lane] = 0.5 * fmin(sc.bnd[nu + lane] - sc.bnd[lane], sc.bnd[3 * nu + lane] - sc.bnd[2 * nu + lane]);
+    const double ln = fabs(lambda[c * nu + lane]);
+    const double wl = sc.wsq ? ln : sqrt(ln);
+    sLw[lane] = wl * wl;
   }
   lds_sync();
   // H(a,b) = sum_i q_i sum_r G_i(r,a) G_i(r,b) + Lambda,  G_i(r, n*Nu + l) = s_in(n1_i + r - l)
@@ -117,11 +125,7 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
       for (; rr < n2; ++rr) a0 += sa[rr] * sb[rr];
       h += sQ[i] * ((a0 + a1) + (a2 + a3));
     }
-    if (a == b) {
-      const double ln = fabs(lambda[c * nu + na]);
-      const double wl = sc.wsq ? ln : sqrt(ln);
-      h += wl * wl;
-    }
+    if (a == b) h += sLw[na];
     sH[a * M + b] = h;
     sH[b * M + a] = h;
   }
@@ -155,8 +159,21 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
       sH[lane * M + k] = lik;
     }
     lds_sync();
-    if (hr && lane > k)
-      for (int j = k + 1; j <= lane; ++j) sH[lane * M + j] -= lik * sH[j * M + k];
+    if (hr && lane > k) {  // four columns' loads before their updates (the stores would otherwise
+                           // hold each next load behind them: one LDS round trip per column)
+      int j = k + 1;
+      for (; j + 3 <= lane; j += 4) {
+        const double h0 = sH[lane * M + j], h1 = sH[lane * M + j + 1];
+        const double h2 = sH[lane * M + j + 2], h3 = sH[lane * M + j + 3];
+        const double l0 = sH[j * M + k], l1 = sH[(j + 1) * M + k];
+        const double l2 = sH[(j + 2) * M + k], l3 = sH[(j + 3) * M + k];
+        sH[lane * M + j] = h0 - lik * l0;
+        sH[lane * M + j + 1] = h1 - lik * l1;
+        sH[lane * M + j + 2] = h2 - lik * l2;
+        sH[lane * M + j + 3] = h3 - lik * l3;
+      }
+      for (; j <= lane; ++j) sH[lane * M + j] -= lik * sH[j * M + k];
+    }
     lds_sync();
   }
   double est = INFINITY;  // a factorisation that fails: treat as heaviest
@@ -211,28 +228,41 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     double e = 0.0;
     for (int k = 0; k < nref; ++k) {
       const double* rk = r + (long long)k * my * nit;
-      for (int t0 = 1; t0 < nit; t0 += kWave) {
-        const int t = t0 + lane;
-        bool jmp = false;
-        if (t < nit)
-          for (int i = 0; i < my; ++i) jmp = jmp || rk[i * nit + t] != rk[i * nit + t - 1];
-        const unsigned long long bal = __ballot(jmp);
-        if (!bal) continue;
-        if (jmp) {
-          const int slot = __popcll(bal & ((1ull << lane) - 1ull));
-          for (int i = 0; i < my; ++i) sD[slot * my + i] = rk[i * nit + t] - rk[i * nit + t - 1];
+      for (int t0 = 1; t0 < nit; t0 += 8 * kWave) {
+        // the jump flags of eight passes first: their loads are independent, so they are issued
+        // together (one global-memory round trip per output instead of one per pass)
+        unsigned jm = 0;
+        for (int i = 0; i < my; ++i) {
+          const double* ri = rk + i * nit;
+#pragma unroll
+          for (int p = 0; p < 8; ++p) {
+            const int t = t0 + p * kWave + lane;
+            const int tc = t < nit ? t : nit - 1;
+            const double a = ri[tc], b = ri[tc - 1];
+            if (t < nit && a != b) jm |= 1u << p;
+          }
         }
-        lds_sync();
-        const int nj = __popcll(bal);
-        for (int p = lane; p < nj * M; p += kWave) {
-          const int j = p / M, m = p - j * M, n = m / nuc;
-          const double bn = 0.5 * fmin(sc.bnd[nu + n] - sc.bnd[n], sc.bnd[3 * nu + n] - sc.bnd[2 * nu + n]);
-          if (!(bn > 0.0 && bn < INFINITY)) continue;
-          double z = 0.0;
-          for (int i = 0; i < my; ++i) z += sD[j * my + i] * sW[i * M + m];
-          e += fabs(z) / bn;
+        for (int p = 0; p < 8; ++p) {
+          const int t = t0 + p * kWave + lane;
+          const bool jmp = (jm >> p) & 1u;
+          const unsigned long long bal = __ballot(jmp);
+          if (!bal) continue;
+          if (jmp) {
+            const int slot = __popcll(bal & ((1ull << lane) - 1ull));
+            for (int i = 0; i < my; ++i) sD[slot * my + i] = rk[i * nit + t] - rk[i * nit + t - 1];
+          }
+          lds_sync();
+          const int nj = __popcll(bal);
+          for (int q = lane; q < nj * M; q += kWave) {
+            const int j = q / M, m = q - j * M, n = m / nuc;
+            const double bn = sBn[n];
+            if (!(bn > 0.0 && bn < INFINITY)) continue;
+            double z = 0.0;
+            for (int i = 0; i < my; ++i) z += sD[j * my + i] * sW[i * M + m];
+            e += fabs(z) / bn;
+          }
+          lds_sync();
         }
-        lds_sync();
       }
     }
     est = wave_sum64(e);
@@ -289,8 +319,8 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   // step-table correlation over the horizon per output and entry) stays small; else weight ratio
   const double hcost = sc ? 0.5 * (double)(sc->nu * sc->numax) * (sc->nu * sc->numax) * sc->my * sc->n2max : 0.0;
   const int Mp = sc ? sc->nu * sc->numax : 0;
-  const size_t lds = sc ? (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my) *
-                                  sizeof(double) + (size_t)sc->my * sizeof(int)
+  const size_t lds = sc ? (size_t)(Mp * Mp + sc->my * Mp + sc->my + sc->my * sc->nu * sc->tlen + kWave * sc->my +
+                                   2 * sc->nu) * sizeof(double) + (size_t)sc->my * sizeof(int)
                         : 0;
   if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && Mp <= 64 &&
       hcost <= kOrderEstMaxCost && lds <= 64 * 1024) {
