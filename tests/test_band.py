@@ -443,8 +443,9 @@ def test_band_config3_grid_costs_against_c_port(gpu):
     """Config-3 cost parity over the grid: the whole 65,536-candidate grid on
     the device against the C restatement's committed costs (tests/golden/config3_cband.npz,
     oracle/cband.c):
-    * every simulation succeeds, and the top-64 ranking under SHELL7_W (Shell7x5.m:202, what the
-      tuner consumes) is identical;
+    * every simulation succeeds, and the ranking under SHELL7_W (Shell7x5.m:202, what the tuner
+      consumes) is identical over its first 3,000 places (measured: the first 3,566, the first
+      difference a pair of candidates 2e-6 apart in F; profiles/r04zr_config3_ranking.json);
     * at most 1.45 % of the candidates' Pareto-weighted costs F = J1 @ SHELL7_W differ by more than
       1e-6 relative (measured 1.34 %, profiles/r04x_config3_rebuild_interval_sweep.jsonl), and at
       most 8.5 % of the stratified sample's per-output J1 (measured 7.80 %);
@@ -472,7 +473,11 @@ def test_band_config3_grid_costs_against_c_port(gpu):
     res = eval_batch(sc, N2, Nu, D, L, r[None], v=v[None])
     assert np.all(res.status == 0), np.unique(res.status, return_counts=True)
     F = res.J1 @ SHELL7_W
-    np.testing.assert_array_equal(np.argsort(F, kind="stable")[:64], np.argsort(d["F_full"], kind="stable")[:64])
+    o_dev, o_ref = np.argsort(F, kind="stable"), np.argsort(d["F_full"], kind="stable")
+    first = np.nonzero(o_dev != o_ref)[0]
+    prefix = int(first[0]) if first.size else F.size
+    print("config3: identical ranking prefix %d" % prefix)
+    assert prefix >= 3000, prefix
     relF = np.abs(F - d["F_full"]) / np.abs(d["F_full"])
     s = config3_stratified(128)
     relJ = np.max(np.abs(res.J1[s] - d["J1_strat"]) / np.abs(d["J1_strat"]), axis=1)
