@@ -1008,7 +1008,7 @@ long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy) {
 
 // One launch per (QP size class MAXM, occupancy class): the dynamic LDS of a launch is what its
 // class's largest simulation needs, so short-horizon candidates are not held to the occupancy of
-// the scenario's (n2_max, nu_max) corner (one workgroup per CU at Shell 7x5's 104 KiB).  Every
+// the scenario's (n2_max, nu_max) corner (one workgroup per CU at Shell 7x5's first 104 KiB).  Every
 // launch spans the whole batch; a simulation runs in the one launch whose class holds its
 // (Mz, LDS bytes) and leaves the others at once (no host round trip to bucket device-resident
 // candidates).  Status-only outcomes (padding, bad horizons) are written by the first launch.
