@@ -423,7 +423,7 @@ def other_workload(args):
         import torch.distributed as tdist
 
         tdist.init_process_group("nccl", device_id=dev)
-    from mpct.dist import band_work_estimate, gather_costs, pad_shard, rank_candidates, shard_indices, shard_indices_keyed
+    from mpct.dist import gather_and_rank, pad_shard, plan_shards
     from mpct.engine import eval_batch_device
 
     v = None
@@ -460,13 +460,9 @@ def other_workload(args):
         cfg = {"workload": "WoodBerry DTC-GPC Monte-Carlo, nit=200, sharded by candidate", "candidates": Cc,
                "draws": D}
     Cg = len(N2)
-    owners = None
-    if args.workload == "shell7x5":
-        # config 3's work varies ~100x over the grid: snake-deal by the a-priori latency estimate
-        owners = [shard_indices_keyed(band_work_estimate(N2, Nu, l), world, k) for k in range(world)]
-        sidx = owners[rank]
-    else:
-        sidx = shard_indices(Cg, world, rank)   # strided: every rank gets the same mix of candidates
+    # config 3's work varies ~100x over the grid: snake-deal by the a-priori latency estimate;
+    # the others strided (every rank gets the same mix of candidates)
+    sidx, owners = plan_shards(N2, Nu, l, world, rank, keyed=args.workload == "shell7x5", nu=sc.nu)
     sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, sidx)
     C = sidx.size
     S = C * nref
@@ -488,9 +484,8 @@ def other_workload(args):
         e1.record(stream)
         if record:
             kev.append((e0, e1))
-        J = out["J1"].view(C, nref, sc.my).amax(dim=1) if nref > 1 else out["J1"]  # worst case over draws
-        costs = gather_costs(J, owners=owners) if dist else J
-        return rank_candidates(costs, tw, Cg)
+        # worst case over the draws (config 4), all-gather, ranking (mpct.dist, gloo-tested)
+        return gather_and_rank(out["J1"], C, nref, tw, Cg, owners=owners, distributed=dist)[1]
 
     steps = args.steps if args.steps != 20 else 2   # a step is a whole grid here (seconds)
     warm = args.warmup if args.warmup != 3 else 1

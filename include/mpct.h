@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-#define MPCT_ABI_VERSION 6 /* 6: strided multi-device shards (mpct_shard_candidates replaces the
+#define MPCT_ABI_VERSION 7 /* 7: every simulation slot is prefilled with MPCT_ST_NOT_RUN and NaN costs
+                              before the class launches (a slot no launch simulates stays so).
+                              6: strided multi-device shards (mpct_shard_candidates replaces the
                               contiguous mpct_shard_range), a device may appear more than once in
                               mpct_eval_batch_multi's list; dims table carries nit, nq.
                               5: one scenario on several GPUs of one process (mpct_eval_batch_multi),
@@ -56,6 +58,9 @@ extern "C" {
 #define MPCT_ST_BADHORIZON 16  /* N2/Nu outside the scenario's range or Nu > N2      */
 #define MPCT_ST_SQP_MAXITER 32 /* NMPC: a Gauss-Newton SQP hit sqp_max at some step  */
 #define MPCT_ST_BOUNDS 64      /* NMPC: the closed loop left the state/OV bounds     */
+#define MPCT_ST_NOT_RUN 128    /* no kernel launch simulated this slot (an internal
+                                  dispatch fault; costs NaN).  Every slot is prefilled
+                                  with it before the class launches, which overwrite it */
 
 /* One SISO discrete transfer function  y = z^-delay * num(z)/den(z) u  in the form tfdata(.,'v')
  * returns it (descending powers of z, numerator padded to the denominator's length, den[0]=1)

@@ -10,5 +10,5 @@ mex('-R2018a', fullfile(repo, 'matlab', 'mpct_mex.c'), ['-I' fullfile(repo, 'inc
     ['-L' csrc], '-lmpct', ['LDFLAGS=$LDFLAGS -Wl,-rpath,' csrc ' -Wl,-rpath,/opt/rocm/lib'], ...
     '-outdir', fullfile(repo, 'matlab'));
 v = mpct_mex('version');
-assert(v >= 6, 'mpct:abi', 'libmpct ABI %d, this MEX needs >= 6', v);
+assert(v >= 7, 'mpct:abi', 'libmpct ABI %d, this MEX needs >= 7', v);
 end

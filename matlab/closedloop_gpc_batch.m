@@ -34,7 +34,7 @@ else
 end
 nref = size(R, 3);
 status = reshape(st, nref, C).';
-bad = any(bitand(status, 2 + 4 + 8 + 16), 2);
+bad = any(bitand(status, 2 + 4 + 8 + 16 + 128), 2);
 J = J1(1:nref:end, :);
 F = nan(C, 1);
 if vns

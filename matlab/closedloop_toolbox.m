@@ -24,7 +24,7 @@ end
 opts = struct('open_loop', 1, 'want_traj', 1);
 [~,~,~,~,status,~,y,u,ys,uopt] = mpct_mex('eval', cache.h, n2, nuh, delta(:).', lambda(:).', r(:, 1:nit), ...
                                           v(:, 1:nit), opts);
-if bitand(status, 2 + 4 + 8 + 16)                  % what sim would have thrown (objectives.FATAL_STATUS)
+if bitand(status, 2 + 4 + 8 + 16 + 128)                  % what sim would have thrown (objectives.FATAL_STATUS)
     error('mpct:sim', 'closed-loop simulation failed (status %d)', status);
 end
 t = (0:nit-1) * Ts;

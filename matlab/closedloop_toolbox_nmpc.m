@@ -30,7 +30,7 @@ end
 opts = struct('open_loop', 1, 'want_traj', 1);
 [~,~,~,~,status,~,y,u,yopt,uopt] = mpct_mex('eval', cache.h, n2, nuh, delta(:).', lambda(:).', ...
                                             r(:, 1:nit), [], opts);
-if bitand(status, 2 + 4 + 8 + 16)
+if bitand(status, 2 + 4 + 8 + 16 + 128)
     error('mpct:nlmpc', 'closed-loop NMPC simulation failed (status %d)', status);
 end
 end

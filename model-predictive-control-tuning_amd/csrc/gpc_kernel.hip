@@ -636,7 +636,8 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const int rs = lo.srow.w ? order_stage(*wo, C * nref, lo.srow.w, &lo.stage, err) : 0;
     if (rs) return rs;
   }
-  int rc = 0;
+  int rc = prefill_results(lo, C * nref, sc.my, sc.nu, stream, err);
+  if (rc) return rc;
   FanScope fs(top_class(maxM) > 16 ? fan : nullptr, stream);
   int k = 0, mlo = 0;
   for (int cls = 16; cls <= top_class(maxM) && rc == 0; cls *= 2) {
@@ -647,7 +648,8 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const hipStream_t st = fs.stream(k);
     const int first = k == 0;
     const bool ext = o.open_loop || o.want_traj;
-    if (cls == 16 && sc.small && !ext) rc = launch_small(sc, C, nref, N2, Nu, delta, lambda, r, o, lo, perm, first, st, err);
+    if (diag_drop_launch(k)) rc = 0;
+    else if (cls == 16 && sc.small && !ext) rc = launch_small(sc, C, nref, N2, Nu, delta, lambda, r, o, lo, perm, first, st, err);
     else if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);

@@ -339,8 +339,11 @@ __global__ void __launch_bounds__(64, 1)
         for (int l = 0; l <= lmax; ++l) a = fma(sp[-l] * sp[-l], snv[n * Nu + l], a);
       }
       const double vu = sob[3 * my + i], vl = sob[2 * my + i], de = snv[M];
-      wrn[2 * g] = (float)rsq_nr(fma(vu * vu, de, a));
-      wrn[2 * g + 1] = (float)rsq_nr(fma(vl * vl, de, a));
+      // a zero normal (a hard bound inside the dead time) keeps norm 1, as the oracle's rn does
+      // (toolbox_band.py band_qp, cband.c): its violation stays visible to the choice and the test
+      const double nu2 = fma(vu * vu, de, a), nl2 = fma(vl * vl, de, a);
+      wrn[2 * g] = nu2 > 0.0 ? (float)rsq_nr(nu2) : 1.0f;
+      wrn[2 * g + 1] = nl2 > 0.0 ? (float)rsq_nr(nl2) : 1.0f;
     }
     lds_sync();
   }
@@ -999,6 +1002,8 @@ __global__ void __launch_bounds__(64, 1)
 #include <algorithm>
 #include <string>
 
+#include "work_order.h"
+
 namespace mpct {
 
 long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy) {
@@ -1046,8 +1051,10 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
         return -3;
       }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, fs.stream(nl++), sc, C, nref, N2,
-                       Nu, delta, lambda, r, v, o, out, mz_lo, lo[k], lds, first ? 1 : 0);
+    const hipStream_t ls = fs.stream(nl);
+    if (!diag_drop_launch(nl++))
+      hipLaunchKernelGGL(kern, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)lds, ls, sc, C, nref, N2, Nu, delta,
+                         lambda, r, v, o, out, mz_lo, lo[k], lds, first ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
@@ -1066,9 +1073,11 @@ int launch_mdband(const DevScenario& sc, long long C, int nref, const int* N2, c
     *err = "nu*nu_max + 1 > 64";
     return -4;
   }
+  int rc = prefill_results(out, C * nref, sc.my, sc.nu, stream, err);
+  if (rc) return rc;
   FanScope fs(fan, stream);
   bool first = true;
-  int nl = 0, rc = 0;
+  int nl = 0;
   if (Mz > 32) rc = launch_band_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, fs, nl, 32, first, err);
   if (rc == 0 && Mz > 16)
     rc = launch_band_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, out, fs, nl, 16, first, err);

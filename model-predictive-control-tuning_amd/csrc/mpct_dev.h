@@ -48,6 +48,7 @@ constexpr int MPCT_ST_SKIPPED_ = 8;
 constexpr int MPCT_ST_BADHORIZON_ = 16;
 constexpr int MPCT_ST_SQP_MAXITER_ = 32;
 constexpr int MPCT_ST_BOUNDS_ = 64;
+constexpr int MPCT_ST_NOT_RUN_ = 128;
 
 // NMPC model parameter table (mpct_nmpc_desc.params, nmpc_vandevusse_state.m:43-58 order)
 enum { NM_K10 = 0, NM_K20, NM_K30, NM_E1, NM_E2, NM_E3, NM_DAB, NM_DBC, NM_DAD, NM_RHO, NM_CP, NM_KW, NM_AR,

@@ -655,6 +655,14 @@ extern "C" int32_t mpct_nmpc_scenario_create(const mpct_nmpc_desc* d, mpct_scena
   if (d->ny < 1 || d->ny > 2) return fail(MPCT_ERANGE, "ny must be 1 or 2");
   if (d->nit < 1 || d->n_max < 1 || d->nu_max < 1) return fail(MPCT_EINVAL, "non-positive dimension");
   if (d->nu * d->nu_max > 32) return fail(MPCT_ERANGE, "nu*nu_max > 32");
+  {
+    // the LDS of every (M, N) a candidate may use (not monotone in N: nm_groups), as the launch checks
+    long long lds_all = 0;
+    for (int m = 1; m <= d->nu * d->nu_max; ++m)
+      for (int n = 1; n <= d->n_max; ++n) lds_all = std::max(lds_all, nmpc_lds_bytes(m, n));
+    if (lds_all > 64 * 1024)
+      return fail(MPCT_ERANGE, "n_max x nu*nu_max needs more than 64 KiB of LDS per simulation");
+  }
   if (!(d->ts > 0.0) || d->nsub < 1) return fail(MPCT_EINVAL, "ts must be > 0 and nsub >= 1");
   if (!d->xc || !d->x0 || !d->u0 || !d->u_min || !d->u_max || !d->x_min || !d->x_max || !d->y_scale ||
       !d->u_scale || !d->yref)

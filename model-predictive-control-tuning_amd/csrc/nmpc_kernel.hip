@@ -170,10 +170,14 @@ __host__ __device__ inline NmLayout nm_layout(int M, int N, int G) {
 }
 
 // point buffers of a simulation: four (one per 16-lane row) when they fit 40 KB, i.e. four
-// workgroups per CU, the one-wave-per-SIMD occupancy of this kernel; else two; the M <= 32 class one
+// workgroups per CU, the one-wave-per-SIMD occupancy of this kernel; else two while they fit the
+// 64 KiB a launch may hold without the MaxDynamicSharedMemorySize opt-in; else one, the single-
+// point pass of the M <= 32 class (long horizons: G = 2 doubles the 3 N M sensitivities, so at
+// nu = 2, N = 127 the M <= 15 class would otherwise need 101 KB against 46 KB for G = 1)
 __host__ __device__ inline int nm_groups(int M, int N) {
   if (M > 15) return 1;
-  return nm_layout(M, N, 4).total * 8 <= 40 * 1024 ? 4 : 2;
+  if (nm_layout(M, N, 4).total * 8 <= 40 * 1024) return 4;
+  return nm_layout(M, N, 2).total * 8 <= 64 * 1024 ? 2 : 1;
 }
 
 // active flags: box rows (p < base) in the lanes' act bits, state-bound rows in an LDS bitmap
@@ -953,9 +957,10 @@ static int launch_nmpc_t(const DevScenario& sc, long long C, int nref, const int
     l = hi[ncls];
   }
   for (int k = ncls - 1; k >= 0; --k) {
-    hipLaunchKernelGGL(nmpc_closed_loop_kernel<MAXM>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)hi[k],
-                       fs.stream(nl++), sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, mz_lo, lo[k], hi[k],
-                       first ? 1 : 0);
+    const hipStream_t ls = fs.stream(nl);
+    if (!diag_drop_launch(nl++))
+      hipLaunchKernelGGL(nmpc_closed_loop_kernel<MAXM>, dim3((unsigned)(C * nref)), dim3(kWave), (size_t)hi[k], ls, sc,
+                         C, nref, N, Nu, delta, lambda, r, perm, o, out, mz_lo, lo[k], hi[k], first ? 1 : 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       *err = std::string("kernel launch failed: ") + hipGetErrorString(e);
@@ -974,7 +979,11 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
     *err = "nu*nu_max > 32";
     return -4;
   }
-  if (nmpc_lds_bytes(Mmax, sc.n2max) > 64 * 1024) {
+  // every (M, N) pair a candidate may use: the layout is not monotone in N (nm_groups)
+  long long lds_all = 0;
+  for (int m = 1; m <= Mmax; ++m)
+    for (int n = 1; n <= sc.n2max; ++n) lds_all = std::max(lds_all, nmpc_lds_bytes(m, n));
+  if (lds_all > 64 * 1024) {
     *err = "n_max x nu*nu_max needs more than 64 KiB of LDS per simulation";
     return -4;
   }
@@ -983,8 +992,10 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
     const int rc0 = order_candidates(kOrderNmpc, sc.my, sc.nu, C, N, Nu, delta, lambda, *wo, &perm, stream, err);
     if (rc0) return rc0;
   }
+  int rc = prefill_results(out, C * nref, sc.my, sc.nu, stream, err);
+  if (rc) return rc;
   FanScope fs(fan, stream);  // forks after the sort: every class launch waits for the permutation
-  int nl = 0, rc = 0;
+  int nl = 0;
   bool first = true;  // the first launch also writes the padding / bad-horizon statuses
   if (Mmax > 15) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 15, first, err);
   if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);

@@ -41,6 +41,14 @@ int order_stage(WorkOrder& wo, long long S, int width, double** stage, std::stri
 int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const StageRow& R,
                       const DevResult& out, hipStream_t stream, std::string* err);
 
+// every simulation slot of `out` (its staging rows when out.stage is set) <- NaN costs, status
+// MPCT_ST_NOT_RUN, 0 iterations; enqueue before the class launches, which overwrite the records
+// of the slots they simulate, so a slot that no launch claims cannot pass for a result
+int prefill_results(const DevResult& out, long long S, int my, int nu, hipStream_t stream, std::string* err);
+// diagnostic: with MPCT_DIAG_DROP_LAUNCH=k in the environment the k-th class launch of every batch
+// is not issued (tests plant the dispatch fault that the prefill must expose); unset, never true
+bool diag_drop_launch(int k);
+
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);
 void order_release(WorkOrder& wo);

@@ -1,6 +1,8 @@
 // work_order.hip — heaviest-first dispatch order of a candidate batch (see work_order.h).
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "wave_ops.h"
 #include "work_order.h"
 
@@ -386,6 +388,54 @@ __global__ void unpermute_kernel(const double* __restrict__ stage, const int* __
     for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = row[R.jnu + i];
   if (R.st >= 0) out.status[s] = (int)row[R.st];
   if (R.it >= 0) out.qp_iters[s] = (long long)row[R.it];
+}
+
+// one thread per simulation slot: NaN costs, status MPCT_ST_NOT_RUN, 0 iterations, in the staging
+// row of the slot (ordered launches) or at the caller's index.  The slot's simulating launch
+// overwrites the whole record; a slot no class launch claims keeps it (VNS2.m:151-163 treats a
+// failed sim as an error, never as a value)
+__global__ void prefill_kernel(DevResult out, long long S, int my, int nu) {
+  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const double nan = __longlong_as_double(0x7ff8000000000000ll);
+  if (out.stage) {
+    const StageRow& R = out.srow;
+    double* row = out.stage + xcd_row(s, S) * R.w;
+    for (int i = 0; i < my; ++i) {
+      if (R.j1 >= 0) row[R.j1 + i] = nan;
+      if (R.j21 >= 0) row[R.j21 + i] = nan;
+      if (R.j22 >= 0) row[R.j22 + i] = nan;
+    }
+    if (R.jnu >= 0)
+      for (int i = 0; i < nu; ++i) row[R.jnu + i] = nan;
+    if (R.st >= 0) row[R.st] = (double)MPCT_ST_NOT_RUN_;
+    if (R.it >= 0) row[R.it] = 0.0;
+    return;
+  }
+  for (int i = 0; i < my; ++i) {
+    if (out.J1) out.J1[s * my + i] = nan;
+    if (out.j21) out.j21[s * my + i] = nan;
+    if (out.j22) out.j22[s * my + i] = nan;
+  }
+  if (out.Jnu)
+    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = nan;
+  if (out.status) out.status[s] = MPCT_ST_NOT_RUN_;
+  if (out.qp_iters) out.qp_iters[s] = 0;
+}
+
+bool diag_drop_launch(int k) {
+  const char* e = getenv("MPCT_DIAG_DROP_LAUNCH");
+  return e && *e && atoi(e) == k;
+}
+
+int prefill_results(const DevResult& out, long long S, int my, int nu, hipStream_t stream, std::string* err) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(prefill_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, out, S, my, nu);
+  if (hipGetLastError() != hipSuccess) {
+    *err = "result prefill launch failed";
+    return -3;
+  }
+  return 0;
 }
 
 int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu, const StageRow& R,

@@ -88,9 +88,9 @@ EXPORTS = [
     "mpct_rank_device",
 ]
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 ST_QP_MAXITER, ST_QP_INFEAS, ST_NONFINITE, ST_SKIPPED, ST_BADHORIZON = 1, 2, 4, 8, 16
-ST_SQP_MAXITER, ST_BOUNDS = 32, 64
+ST_SQP_MAXITER, ST_BOUNDS, ST_NOT_RUN = 32, 64, 128
 NMPC_VANDEVUSSE = 1
 
 _lib = None

@@ -114,3 +114,36 @@ def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = 
     s = costs @ weights
     s = torch.where(torch.isnan(s), torch.full_like(s, float("inf")), s)
     return torch.argsort(s, stable=True)
+
+
+def plan_shards(N2, Nu, lam, world: int, rank: int, keyed: bool = False, nu: int = 3):
+    """The candidates rank scores and the owners table gather_costs needs: strided shards (owners
+    None), or, keyed (config 3, whose per-simulation latency varies ~100x over the grid), the snake
+    deal of shard_indices_keyed by band_work_estimate with every rank's owners (identical on every
+    rank, so the gathered rows land in the grid's order).  Returns (idx, owners)."""
+    if keyed:
+        work = band_work_estimate(N2, Nu, lam, nu)
+        owners = [shard_indices_keyed(work, world, k) for k in range(world)]
+        return owners[rank], owners
+    return shard_indices(len(N2), world, rank), None
+
+
+def worst_over_draws(J: torch.Tensor, n: int, nref: int) -> torch.Tensor:
+    """Per-candidate cost of a Monte-Carlo batch (config 4): the plant-mismatch draws of one
+    candidate ride the reference dimension (simulation s = c*nref + k, DTC_GPC_WW.m:18-19 with one
+    mismatched plant per draw) and so sit on the candidate's rank; its record is the worst case over
+    them, per output.  A failed or sentinel draw (NaN) makes the candidate's record NaN."""
+    if nref == 1:
+        return J
+    return J.view(n, nref, J.shape[-1]).amax(dim=1)
+
+
+def gather_and_rank(J: torch.Tensor, n: int, nref: int, weights: torch.Tensor, C: int, owners=None,
+                    distributed: bool = True):
+    """The data-parallel epilogue of one scoring step: the rank's simulation records J [n*nref, K]
+    -> per-candidate records (worst_over_draws) -> one all-gather (gather_costs, owners as
+    plan_shards returns them) -> the ranking every rank computes (rank_candidates) over the C real
+    candidates.  Returns (gathered records [>= C, K], order [C])."""
+    local = worst_over_draws(J, n, nref)
+    costs = gather_costs(local, owners=owners) if distributed else local
+    return costs, rank_candidates(costs, weights, C)

@@ -14,16 +14,17 @@ from __future__ import annotations
 
 import numpy as np
 
-from ._lib import ST_BADHORIZON, ST_NONFINITE, ST_QP_INFEAS, ST_SKIPPED
+from ._lib import ST_BADHORIZON, ST_NONFINITE, ST_NOT_RUN, ST_QP_INFEAS, ST_SKIPPED
 from .engine import eval_batch
 from .scenarios import vns_step_refs
 
 # A simulation is unusable only when the reference's sim/nlmpcmove would have thrown (caught and
 # skipped with fprintf, VNS2.m:161-163, GAM_fun.m:82-84) or produced no trajectory: an infeasible
-# QP, a non-finite state, a skipped or invalid candidate.  An iteration cap (QP_MAXITER, NMPC
+# QP, a non-finite state, a skipped or invalid candidate -- or a slot that no kernel launch
+# simulated (ST_NOT_RUN, an internal dispatch fault: its costs are the prefill's NaN).  An iteration cap (QP_MAXITER, NMPC
 # SQP_MAXITER) or an NMPC closed loop that grazed its state bounds keeps the last iterate and a
 # finite cost, as mpcmove / nlmpcmove do (closedloop_toolbox_nmpc.m:69 uses the last iterate).
-FATAL_STATUS = ST_QP_INFEAS | ST_NONFINITE | ST_SKIPPED | ST_BADHORIZON
+FATAL_STATUS = ST_QP_INFEAS | ST_NONFINITE | ST_SKIPPED | ST_BADHORIZON | ST_NOT_RUN
 
 
 def failed(status) -> np.ndarray:

@@ -16,6 +16,7 @@ the HIP engine (mpct.engine, the product path) or by a checker in tests.
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 from dataclasses import dataclass, field
@@ -227,7 +228,8 @@ class StaleRows:
         ok = np.asarray(ok, dtype=bool)
         self.last[ok] = terms[ok]
         if ok[0]:
-            self.row1 = bcast
+            self.row1 = bcast  # evaluated below only while row 1 is the only row (memoized per
+            # neighbour by its producer, batch_vns_rows, so a cache hit does not re-simulate)
         if ok.any():
             self.nrows = max(self.nrows, int(np.nonzero(ok)[0].max()) + 1)
         if self.nrows < self.last.size:
@@ -573,8 +575,13 @@ def engine_evaluators(sc, r, par: TuningPar, device: int = -1, vns_refs=None, md
         T = j21 + j22 + jnu
 
         def bcast(key):
-            return lambda: vns_row1_broadcast(sc, max(key[0]), max(key[1]), delta, lam, device=device,
-                                              refs=vns_refs, mdv=mdv)
+            # evaluated at most once per neighbour: the callable rides in vns2_batched's cache entry,
+            # so every later score of that neighbour (cache hits, replays) reuses the value
+            @functools.lru_cache(maxsize=1)
+            def term():
+                return vns_row1_broadcast(sc, max(key[0]), max(key[1]), delta, lam, device=device,
+                                          refs=vns_refs, mdv=mdv)
+            return term
         return [(T[k], ~bad[k], bcast(keys[k])) for k in range(len(keys))]
 
     batch_vns.rows = batch_vns_rows if my == ny else None

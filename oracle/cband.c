@@ -50,6 +50,10 @@ typedef struct {
   const double* su;   /* [nu] MV ScaleFactor */
   double rho;         /* Weights.ECR */
   const double* yref; /* [my][nit] */
+  int qp_warm;        /* 1: a second, equally valid QP path -- each step's dual method starts from
+                         the previous step's final active set (re-solved exactly on it, negative
+                         multipliers dropped) instead of from the unconstrained minimum.  The
+                         C-vs-C floor of the config-3 parity (tools/config3_certify.py) */
 } cb_scen;
 
 /* status bits (same meaning as the device's) */
@@ -161,13 +165,60 @@ static void apply_q(const dual_t* D, int q, double* y) {
 
 #define RQ(D, r, c) ((D)->Rq[(size_t)(c) * (D)->Mp + (r)])
 
-/* w solves min 1/2|w + gw|^2 s.t. Aw w >= bw.  Returns iterations; status bits in *st. */
-static int dual_solve(dual_t* D, double* w, double tol, int maxit, int* st) {
+/* exact solve on the active set act[0..q): w = -gw + Q1 R^-T (b_A + Aw_A gw), u = R^-1 y (raw) */
+static void resolve_active(dual_t* D, int q, double* w, double* u) {
+  const int Mp = D->Mp;
+  double y[CB_MAXMP], z[CB_MAXMP];
+  qr_active(D, q);
+  for (int j = 0; j < q; ++j) {
+    const double* aj = D->Aw + (size_t)D->act[j] * Mp;
+    double acc = D->bw[D->act[j]];
+    for (int m = 0; m < Mp; ++m) acc += aj[m] * D->gw[m];
+    for (int i = 0; i < j; ++i) acc -= RQ(D, i, j) * y[i];
+    y[j] = acc / RQ(D, j, j);
+  }
+  memset(z, 0, sizeof(double) * Mp);
+  memcpy(z, y, sizeof(double) * q);
+  apply_q(D, q, z);
+  for (int m = 0; m < Mp; ++m) w[m] = -D->gw[m] + z[m];
+  for (int j = q - 1; j >= 0; --j) {
+    double acc = y[j];
+    for (int i = j + 1; i < q; ++i) acc -= RQ(D, j, i) * u[i];
+    u[j] = acc / RQ(D, j, j);
+  }
+}
+
+/* w solves min 1/2|w + gw|^2 s.t. Aw w >= bw.  Returns iterations; status bits in *st.
+ * q0 > 0: warm start from the active rows D->act[0..q0) (cb_scen.qp_warm): exact solve on them,
+ * the most negative multiplier dropped until none is, then the ordinary dual iterations.  *qout:
+ * the final active-set size (D->act[0..*qout)) */
+static int dual_solve(dual_t* D, double* w, double tol, int maxit, int* st, int q0, int* qout) {
   const int Mp = D->Mp, nrow = D->nrow;
-  double u[CB_MAXMP + 1], up[CB_MAXMP + 1], z[CB_MAXMP], qn[CB_MAXMP], r[CB_MAXMP], y[CB_MAXMP];
+  double u[CB_MAXMP + 1], up[CB_MAXMP + 1], z[CB_MAXMP], qn[CB_MAXMP], r[CB_MAXMP];
   unsigned char* isact = (unsigned char*)calloc((size_t)nrow, 1);
   int q = 0, it = 0;
   for (int m = 0; m < Mp; ++m) w[m] = -D->gw[m];
+  if (q0 > 0) {
+    q = q0;
+    for (int j = 0; j < q; ++j) isact[D->act[j]] = 1;
+    while (q > 0) {
+      resolve_active(D, q, w, u);
+      int k = -1;
+      double umin = 0.0;
+      for (int j = 0; j < q; ++j)
+        if (u[j] < umin) {
+          umin = u[j];
+          k = j;
+        }
+      if (k < 0) break;
+      ++it;
+      isact[D->act[k]] = 0;
+      for (int j = k; j < q - 1; ++j) D->act[j] = D->act[j + 1];
+      --q;
+    }
+    if (q == 0)
+      for (int m = 0; m < Mp; ++m) w[m] = -D->gw[m];
+  }
   for (;;) {
     int p = -1;
     double best = INFINITY;
@@ -235,24 +286,8 @@ static int dual_solve(dual_t* D, double* w, double tol, int maxit, int* st) {
       if (t2 <= t1) {
         D->act[q++] = p;
         isact[p] = 1;
-        /* exact re-solve on the active set: w = -gw + Q1 R^-T (b_A + Aw_A gw), u = R^-1 y */
-        qr_active(D, q);
-        for (int j = 0; j < q; ++j) {
-          const double* aj = D->Aw + (size_t)D->act[j] * Mp;
-          double acc = D->bw[D->act[j]];
-          for (int m = 0; m < Mp; ++m) acc += aj[m] * D->gw[m];
-          for (int i = 0; i < j; ++i) acc -= RQ(D, i, j) * y[i];
-          y[j] = acc / RQ(D, j, j);
-        }
-        memset(z, 0, sizeof(double) * Mp);
-        memcpy(z, y, sizeof(double) * q);
-        apply_q(D, q, z);
-        for (int m = 0; m < Mp; ++m) w[m] = -D->gw[m] + z[m];
-        for (int j = q - 1; j >= 0; --j) {
-          double acc = y[j];
-          for (int i = j + 1; i < q; ++i) acc -= RQ(D, j, i) * u[i];
-          u[j] = acc / RQ(D, j, j);
-        }
+        /* exact re-solve on the active set */
+        resolve_active(D, q, w, u);
         for (int j = 0; j < q; ++j) u[j] = fmax(u[j], 0.0);
         break;
       }
@@ -280,6 +315,7 @@ out:
     if (smin < -1e-9) *st |= CB_ST_SLACK;
   }
   free(isact);
+  if (qout) *qout = q;
   return it;
 }
 
@@ -293,9 +329,14 @@ typedef struct {
   double* Ls;     /* [Mp][Mp] lower Cholesky factor of Hs */
   double* dsc;    /* [Mp] */
   double* rn;     /* [nrow] row norms of A*dsc */
-  int* rkind;     /* [nrow] 0 du_min, 1 du_max, 2 u_min, 3 u_max, 4 eps, 5 y_max, 6 y_min */
-  int* rarg;      /* [nrow] move index m (kinds 0-3) or (i*N2 + k) (kinds 5-6) */
+  int* rkind;     /* [nrow] 0 du_min, 1 du_max, 2 u_min, 3 u_max, 4 eps, 5 y_max, 6 y_min,
+                     7 / 8 du_n(0) >= / <= a pinned value (replay-gap mode only, last 2 nu rows) */
+  int* rarg;      /* [nrow] move index m (kinds 0-3, 7-8) or (i*N2 + k) (kinds 5-6) */
   double* wq;     /* [my] */
+  double wl[64];  /* [nu] move weights */
+  int warm, q_prev; /* qp_warm: the previous QP's final active-set size (D.act[0..q_prev)) */
+  int pin_on;       /* pin rows enforce pin[] (else their bounds are -inf: never violated) */
+  double pin[64];
   dual_t D;
 } cand_t;
 
@@ -322,7 +363,9 @@ static void cand_free(cand_t* c) {
 static void a_row(const cand_t* c, const cb_scen* sc, int kind, int arg, double* a) {
   const int M = c->M, Nu = c->Nu;
   memset(a, 0, sizeof(double) * c->Mp);
-  if (kind <= 3) {
+  if (kind >= 7) {
+    a[arg] = kind == 7 ? 1.0 : -1.0;
+  } else if (kind <= 3) {
     int n = arg / Nu;
     if (kind == 0) a[arg] = 1.0;
     else if (kind == 1) a[arg] = -1.0;
@@ -340,7 +383,7 @@ static void a_row(const cand_t* c, const cb_scen* sc, int kind, int arg, double*
 }
 
 static int cand_setup(cand_t* c, const cb_scen* sc, int N2, int Nu, const double* delta, const double* lam,
-                      double* wl) {
+                      double* wl, int pin_rows) {
   const int my = sc->my, nu = sc->nu, nin = sc->nu + sc->nd;
   memset(c, 0, sizeof(*c));
   c->my = my;
@@ -364,7 +407,9 @@ static int cand_setup(cand_t* c, const cb_scen* sc, int N2, int Nu, const double
   for (int n = 0; n < nu; ++n) {
     double l = fabs(lam[n]) / sc->su[n];
     wl[n] = sc->wsq ? l * l : l;
+    c->wl[n] = wl[n];
   }
+  c->warm = sc->qp_warm;
   /* step table and G (toolbox_band.py:97-113) */
   double* S = (double*)malloc(sizeof(double) * (N2 + 2));
   c->G = (double*)calloc((size_t)my * N2 * M, sizeof(double));
@@ -419,7 +464,7 @@ static int cand_setup(cand_t* c, const cb_scen* sc, int N2, int Nu, const double
   }
   free(H);
   /* constraint rows in toolbox_band.py:284-298 order */
-  int cap = 4 * M + 1 + 2 * my * N2;
+  int cap = 4 * M + 1 + 2 * my * N2 + 2 * nu;
   c->rkind = (int*)malloc(sizeof(int) * cap);
   c->rarg = (int*)malloc(sizeof(int) * cap);
   int nr = 0;
@@ -446,6 +491,12 @@ static int cand_setup(cand_t* c, const cb_scen* sc, int N2, int Nu, const double
         c->rarg[nr++] = i * N2 + k;
       }
   }
+  if (pin_rows)
+    for (int n = 0; n < nu; ++n)
+      for (int kind = 7; kind <= 8; ++kind) {
+        c->rkind[nr] = kind;
+        c->rarg[nr++] = n * Nu;
+      }
   c->nrow = nr;
   /* Aw = (A D / rn) Ls^-T: row-wise forward substitution with Ls */
   c->rn = (double*)malloc(sizeof(double) * nr);
@@ -514,12 +565,14 @@ static int cand_qp(cand_t* c, const cb_scen* sc, const double* f, const double* 
       case 3: b = -(sc->bnd[3 * nu + n] - up[n]); break;
       case 4: b = 0.0; break;
       case 5: b = f[arg] - sc->ymax[arg / N2]; break;
-      default: b = sc->ymin[arg / N2] - f[arg]; break;
+      case 6: b = sc->ymin[arg / N2] - f[arg]; break;
+      case 7: b = c->pin_on ? c->pin[n] : -INFINITY; break;
+      default: b = c->pin_on ? -c->pin[n] : -INFINITY; break;
     }
     D->bw[r] = b / c->rn[r];
   }
   double w[CB_MAXMP];
-  int it = dual_solve(D, w, 1e-12, 5000, st);
+  int it = dual_solve(D, w, 1e-12, 5000, st, c->warm ? c->q_prev : 0, &c->q_prev);
   /* x = D Ls^-T w */
   for (int m = Mp - 1; m >= 0; --m) {
     double acc = w[m];
@@ -529,6 +582,24 @@ static int cand_qp(cand_t* c, const cb_scen* sc, const double* f, const double* 
   for (int m = 0; m < Mp; ++m) x[m] *= c->dsc[m];
   (void)M;
   return it;
+}
+
+/* the QP objective 1/2 |W x + c|^2 at x = [dU; eps] (toolbox_band.py band_qp with_obj) */
+static double cand_obj(const cand_t* c, const cb_scen* sc, const double* f, const double* rv, const double* x) {
+  const int M = c->M, N2 = c->N2;
+  double J = 0.0;
+  for (int i = 0; i < c->my; ++i) {
+    if (!(c->wq[i] > 0)) continue;
+    for (int k = 0; k < N2; ++k) {
+      const double* g = c->G + (size_t)(i * N2 + k) * M;
+      double e = f[i * N2 + k] - rv[i];
+      for (int m = 0; m < M; ++m) e += g[m] * x[m];
+      J += c->wq[i] * e * e;
+    }
+  }
+  for (int m = 0; m < M; ++m) J += c->wl[m / c->Nu] * x[m] * x[m];
+  J += sc->rho * x[M] * x[M];
+  return 0.5 * J;
 }
 
 /* history input of column j at time tau: before t the applied signal, from t on the held value */
@@ -591,11 +662,11 @@ static void step_plant(const cand_t* c, const double* U, double* Ye, int t, int 
 static int simulate(const cb_scen* sc, int N2, int Nu, const double* delta, const double* lam, const double* r,
                     const double* v, int open_loop, const double* Uforce, int T, double* du_o, double* J1,
                     double* j21, double* j22, double* Jnu, int64_t* iters_out, double* ytraj, double* utraj,
-                    double* ystraj, double* uopttraj) {
+                    double* ystraj, double* uopttraj, double* gap_free, double* gap_pin) {
   const int my = sc->my, nu = sc->nu, nd = sc->nd, nin = nu + nd, nit = sc->nit;
   double wl[64];
   cand_t c;
-  int st = cand_setup(&c, sc, N2, Nu, delta, lam, wl);
+  int st = cand_setup(&c, sc, N2, Nu, delta, lam, wl, gap_pin != NULL);
   int64_t iters = 0;
   if (st) {
     cand_free(&c);
@@ -685,6 +756,18 @@ static int simulate(const cb_scen* sc, int N2, int Nu, const double* delta, cons
     for (int i = 0; i < my; ++i) rv[i] = r[(size_t)i * nit + t];
     free_response(&c, U, Ye, t, nT, up, vt, f, yq);
     iters += cand_qp(&c, sc, f, rv, up, x, &st);
+    if (Uforce && gap_pin) {
+      /* replay gap (toolbox_band.py pinned_gap): the objective at the free optimum, and the
+       * optimum with every MV's first move pinned to the applied one */
+      double xp[CB_MAXMP];
+      gap_free[t] = cand_obj(&c, sc, f, rv, x);
+      for (int n = 0; n < nu; ++n) c.pin[n] = Uforce[(size_t)n * nit + t] - up[n];
+      int stp = 0; /* a failed pinned QP marks its step (NaN), not the replay */
+      c.pin_on = 1;
+      cand_qp(&c, sc, f, rv, up, xp, &stp);
+      c.pin_on = 0;
+      gap_pin[t] = stp ? NAN : cand_obj(&c, sc, f, rv, xp);
+    }
     for (int n = 0; n < nu; ++n) {
       double un;
       if (Uforce) {
@@ -737,7 +820,7 @@ int cband_eval(const cb_scen* sc, int64_t C, const int* N2, const int* Nu, const
                          v + (size_t)k * nd * nit, open_loop, NULL, 0, NULL, J1 + s * my, j21 + s * my,
                          j22 + s * my, Jnu + s * nu, iters + s, ytraj ? ytraj + (size_t)s * my * nit : 0,
                          utraj ? utraj + (size_t)s * nu * nit : 0, ystraj ? ystraj + (size_t)s * my * nit : 0,
-                         uopttraj ? uopttraj + (size_t)s * nu * nit : 0);
+                         uopttraj ? uopttraj + (size_t)s * nu * nit : 0, NULL, NULL);
   }
   return 0;
 }
@@ -755,6 +838,27 @@ int cband_replay(const cb_scen* sc, int64_t C, const int* N2, const int* Nu, con
 #endif
   for (int64_t c = 0; c < C; ++c)
     status[c] = simulate(sc, N2[c], Nu[c], delta + c * my, lam + c * nu, r, v, 0, U + (size_t)c * nu * nit, T,
-                         du_o + (size_t)c * nu * T, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
+                         du_o + (size_t)c * nu * T, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL,
+                         NULL, NULL);
+  return 0;
+}
+
+/* The replay plus, at every step t < T, toolbox_band.py pinned_gap's two objectives: gap_free
+ * [C][T] at the oracle's optimum of the state the trajectory reached, gap_pin [C][T] with every
+ * MV's first move pinned to the applied one.  A move that differs from the oracle's yet attains
+ * its optimal cost is an equally optimal solution of a flat QP. */
+int cband_replay_gap(const cb_scen* sc, int64_t C, const int* N2, const int* Nu, const double* delta,
+                     const double* lam, const double* r, const double* v, const double* U, int T, int nthreads,
+                     double* du_o, double* gap_free, double* gap_pin, int* status) {
+  const int my = sc->my, nu = sc->nu, nit = sc->nit;
+  if (T < 0 || T > nit) return -1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int64_t c = 0; c < C; ++c)
+    status[c] = simulate(sc, N2[c], Nu[c], delta + c * my, lam + c * nu, r, v, 0, U + (size_t)c * nu * nit, T,
+                         du_o + (size_t)c * nu * T, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL,
+                         gap_free + (size_t)c * T, gap_pin + (size_t)c * T);
   return 0;
 }

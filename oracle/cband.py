@@ -22,7 +22,7 @@ class CbScen(C.Structure):
                 ("wsq", C.c_int), ("ink0", C.c_int), ("maxb", C.c_int), ("maxa", C.c_int),
                 ("nb", _ip), ("na", _ip), ("b", _dp), ("a", _dp), ("bnd", _dp),
                 ("ymin", _dp), ("ymax", _dp), ("ecrmin", _dp), ("ecrmax", _dp), ("sy", _dp),
-                ("su", _dp), ("rho", C.c_double), ("yref", _dp)]
+                ("su", _dp), ("rho", C.c_double), ("yref", _dp), ("qp_warm", C.c_int)]
 
 
 def _load():
@@ -35,13 +35,18 @@ def _load():
     lib.cband_replay.restype = C.c_int
     lib.cband_replay.argtypes = [C.POINTER(CbScen), C.c_int64] + [C.c_void_p] * 7 + [
         C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    lib.cband_replay_gap.restype = C.c_int
+    lib.cband_replay_gap.argtypes = [C.POINTER(CbScen), C.c_int64] + [C.c_void_p] * 7 + [
+        C.c_int, C.c_int] + [C.c_void_p] * 4
     return lib
 
 
 class CBand:
     """C port of ``toolbox_band.closedloop_band`` / ``replay_moves`` for one BandScenario."""
 
-    def __init__(self, sc, nit, yref, ink=10):
+    def __init__(self, sc, nit, yref, ink=10, warm=False):
+        """warm: the second, equally valid QP path (each step's dual method warm-started from the
+        previous step's final active set; cband.c cb_scen.qp_warm) -- the C-vs-C floor."""
         self.lib = _load()
         my, nu, nin = sc.my, sc.nu, sc.nin
         ba = [sc.plant[i][j].zinv_form() for i in range(my) for j in range(nin)]
@@ -70,6 +75,7 @@ class CBand:
         for k in ("b", "a", "bnd", "ymin", "ymax", "ecrmin", "ecrmax", "sy", "su", "yref"):
             setattr(s, k, self.t[k].ctypes.data_as(_dp))
         s.rho = float(sc.rho)
+        s.qp_warm = int(bool(warm))
         self.s = s
         self.my, self.nu, self.nd, self.nit = my, nu, nin - nu, int(nit)
 
@@ -121,3 +127,24 @@ class CBand:
             raise ValueError("cband_replay: bad T")
         du_a = np.diff(np.concatenate([np.zeros((N2.size, self.nu, 1)), U], axis=2), axis=2)[:, :, :T]
         return du_o, du_a, st
+
+    def replay_gap(self, N2, Nu, delta, lam, r, v, U, T=None, threads=0):
+        """replay() plus toolbox_band.pinned_gap at every step: (du_o (C, nu, T), du_a, J_free
+        (C, T), J_pinned (C, T), status).  J_pinned is NaN where the pinned QP failed."""
+        N2, Nu, delta, lam = self._cands(N2, Nu, delta, lam)
+        nit = self.nit
+        T = nit if T is None else int(T)
+        U = np.ascontiguousarray(np.asarray(U, float).reshape(N2.size, self.nu, nit))
+        r = np.ascontiguousarray(np.asarray(r, float).reshape(self.my, nit))
+        v = np.ascontiguousarray(np.asarray(v, float).reshape(self.nd, nit))
+        du_o = np.zeros((N2.size, self.nu, T))
+        J0 = np.zeros((N2.size, T))
+        J1 = np.zeros((N2.size, T))
+        st = np.zeros(N2.size, np.int32)
+        rc = self.lib.cband_replay_gap(C.byref(self.s), N2.size, N2.ctypes.data, Nu.ctypes.data, delta.ctypes.data,
+                                       lam.ctypes.data, r.ctypes.data, v.ctypes.data, U.ctypes.data, T, int(threads),
+                                       du_o.ctypes.data, J0.ctypes.data, J1.ctypes.data, st.ctypes.data)
+        if rc != 0:
+            raise ValueError("cband_replay_gap: bad T")
+        du_a = np.diff(np.concatenate([np.zeros((N2.size, self.nu, 1)), U], axis=2), axis=2)[:, :, :T]
+        return du_o, du_a, J0, J1, st

@@ -232,11 +232,16 @@ def cost(x, U, u_last, rvec, N, Nu, wy, wu):
     return 0.5 * float(np.sum(((Y - rvec[None, :]) * wy[None, :]) ** 2) + np.sum((du * wu[None, :]) ** 2))
 
 
-def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None):
+def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None, return_step=False):
     """One nlmpcmove restated (see module docstring).  xbounds = (x_min, x_max): hard state
     bounds (VanDeVusse_NMPC.m:143-146; the OV bounds of :139-142 are the same limits on states
     2:3, softened, so the hard ones dominate), linearised along the prediction in every
-    Gauss-Newton subproblem.  Returns (U, iterations)."""
+    Gauss-Newton subproblem.  Returns (U, iterations).
+
+    On convergence (max |d| / s_u <= SQP_TOL) the iterate v is returned.  return_step=True
+    returns clip(v + d) instead, the convention of rounds 1-3.  Which of the two nlmpcmove's
+    fmincon returns is not public and no fixture pins it: parity unpinned.  The two
+    differ by at most SQP_TOL s_u in one call; tests/test_nmpc.py bounds their closed-loop drift."""
     from scipy.optimize import lsq_linear
 
     from .toolbox_band import qp_dual_dense
@@ -294,6 +299,8 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None):
             # converged: the iterate itself is returned (not v + d, |d| <= SQP_TOL s_u), so the
             # device can run the next call's first prediction from it alongside its last trial
             # pass (nmpc_kernel.hip mpass)
+            if return_step:
+                U = np.clip(v + d, np.repeat(LB, Nu), np.repeat(UB, Nu)).reshape(NU, Nu).T.copy()
             break
         # Armijo backtracking on the cost along the Gauss-Newton step: pure Gauss-Newton 2-cycles
         # on the large-residual steps of this reactor (e.g. after the setpoint change)
@@ -333,7 +340,7 @@ def controller(x, u_last, rvec, N, Nu, delta, lam, U_init, xbounds=None):
 
 
 def closedloop_nmpc(r, N: int, Nu: int, delta, lam, nit: int = NIT, x0=None, u0=U0,
-                    open_loop: bool = True, xbounds=(XMIN, XMAX)) -> NMPCResult:
+                    open_loop: bool = True, xbounds=(XMIN, XMAX), return_step: bool = False) -> NMPCResult:
     """[y,u,yopt,uopt] = closedloop_toolbox_nmpc(nmpcobj,model,init,r,N,Nu,delta,lambda,nit)."""
     x0 = steady_state() if x0 is None else np.asarray(x0, dtype=float)
     r = np.asarray(r, dtype=float).reshape(NY, nit)
@@ -346,7 +353,7 @@ def closedloop_nmpc(r, N: int, Nu: int, delta, lam, nit: int = NIT, x0=None, u0=
     Uw = np.tile(np.asarray(u0, dtype=float), (Nu, 1))
     iters = 0
     for i in range(1, nit):
-        Uw, it = controller(X[:, i - 1], U[:, i - 1], r[:, i], N, Nu, delta, lam, Uw, xbounds)
+        Uw, it = controller(X[:, i - 1], U[:, i - 1], r[:, i], N, Nu, delta, lam, Uw, xbounds, return_step)
         iters += it
         U[:, i] = Uw[0]
         X[:, i] = rk4(X[:, i - 1], U[:, i])
@@ -357,7 +364,7 @@ def closedloop_nmpc(r, N: int, Nu: int, delta, lam, nit: int = NIT, x0=None, u0=
     yopt = uopt = None
     if open_loop:
         Uo, it = controller(x0, np.asarray(u0, dtype=float), r[:, -1], N, Nu, delta, lam,
-                            np.tile(np.asarray(u0, dtype=float), (Nu, 1)), xbounds)
+                            np.tile(np.asarray(u0, dtype=float), (Nu, 1)), xbounds, return_step)
         iters += it
         # MVopt: p+1 rows (moves held after Nu), padded with its last row to nit
         uo = np.array([Uo[min(k, Nu - 1)] for k in range(nit)])

@@ -35,7 +35,7 @@ def test_header_and_exports_agree(built):
 def test_abi_version(built):
     from mpct import _lib
 
-    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.load().mpct_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_abi_v1_descriptor_accepted(built, monkeypatch):

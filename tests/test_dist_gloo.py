@@ -117,3 +117,127 @@ def test_config3_strided_shards_are_balanced():
         assert max(per_rank) / np.mean(per_rank) == 1.0
         contiguous = [work[r * N2.size // W:(r + 1) * N2.size // W].sum() for r in range(W)]
         assert max(contiguous) / np.mean(contiguous) > 1.3
+
+
+# ---- bench.py's config-3 and config-4 multi-rank logic: mpct.dist.plan_shards
+# (keyed owners for config 3, strided otherwise), worst_over_draws (config 4's plant-mismatch draws
+# co-located on the candidate's rank) and gather_and_rank, with C-restatement costs standing in
+def _c3_subgrid():
+    """Nine light config-3 grid candidates (N2 <= 24, Nu <= 2: the C port scores them in ms) with
+    the measured disturbances of Shell7x5.m."""
+    from mpct.scenarios import config3_grid
+
+    N2, Nu, D, L = config3_grid(1024)
+    pick = np.nonzero((N2 <= 24) & (Nu <= 2))[0][::997][:9]
+    return N2[pick], Nu[pick], D[pick], L[pick]
+
+
+def _c3_costs(N2, Nu, d, l):
+    """per-output J1 of config-3 candidates by oracle/cband.c with the measured disturbance v; NaN
+    rows for sentinels (N2 == 0), like the kernel's status-8 records"""
+    from oracle.cband import CBand
+    from oracle.scenarios import shell7x5
+
+    osc, r, v, yref, fx = shell7x5()
+    out = np.full((len(N2), 7), np.nan)
+    ok = N2 > 0
+    if ok.any():
+        out[ok] = CBand(osc, 200, yref).eval(N2[ok], Nu[ok], d[ok], l[ok], r[None], v[None], threads=1)["J1"]
+    return out
+
+
+C4_DRAWS = 3
+
+
+def _c4_grid():
+    from mpct.dtc import config4_candidates
+
+    N2, Nu, d, l = config4_candidates(40)
+    pick = np.nonzero((N2 <= 10) & (Nu <= 3))[0][:5]
+    return N2[pick], Nu[pick], d[pick], l[pick]
+
+
+def _c4_costs(N2, Nu, d, l):
+    """[n * draws, 2] simulation records s = c*draws + k: J1 of oracle/dtcgpc.py dtc_gpc_ww
+    (DTC_GPC_WW.m's loop) with Monte-Carlo plant draw k; NaN for sentinels"""
+    from oracle.dtcgpc import dtc_gpc_ww, woodberry_mc_draws
+
+    plants = woodberry_mc_draws(C4_DRAWS)
+    out = np.full((len(N2) * C4_DRAWS, 2), np.nan)
+    for c in range(len(N2)):
+        if N2[c] <= 0:
+            continue
+        for k in range(C4_DRAWS):
+            p, m = int(N2[c]), int(Nu[c])
+            o = dtc_gpc_ww(p=(p, p), m=(m, m), lam=tuple(l[c]), delta=tuple(d[c]), plant=plants[k])
+            out[c * C4_DRAWS + k] = ((o["y"] - o["r"]) ** 2).sum(1)
+    return out
+
+
+def _cfg_worker(rank, world, port, cfg, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpct.dist import gather_and_rank, pad_shard, plan_shards
+        from mpct.scenarios import SHELL7_W
+
+        if cfg == "shell7x5":
+            N2, Nu, d, l = _c3_subgrid()
+            costs, nref, w = _c3_costs, 1, SHELL7_W
+        else:
+            N2, Nu, d, l = _c4_grid()
+            costs, nref, w = _c4_costs, C4_DRAWS, np.ones(2)
+        idx, owners = plan_shards(N2, Nu, l, world, rank, keyed=cfg == "shell7x5")
+        sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, idx)
+        J = torch.from_numpy(costs(sN2, sNu, sd, sl))
+        g, order = gather_and_rank(J, idx.size, nref, torch.tensor(w, dtype=torch.float64), len(N2), owners=owners)
+        q.put((rank, idx, None if owners is None else [o.tolist() for o in owners], g.numpy(), order.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["shell7x5", "dtc-mc"])
+def test_two_rank_bench_workloads(built, cfg):
+    """bench.py's multi-rank paths of configs 3 and 4 at world size 2 over gloo: config 3's keyed
+    owners (band_work_estimate snake deal, measured disturbances in every simulation) and config 4's
+    draws co-located on their candidate's rank with the worst case over draws.  Every rank holds
+    bit-identical gathered records equal to the single-process costs, NaN sentinel padding, and the
+    same ranking as a single process."""
+    from mpct.dist import band_work_estimate, shard_indices_keyed
+    from mpct.scenarios import SHELL7_W
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got.sort(key=lambda t: t[0])
+    if cfg == "shell7x5":
+        N2, Nu, d, l = _c3_subgrid()
+        ref, w = _c3_costs(N2, Nu, d, l), SHELL7_W
+        owners = [shard_indices_keyed(band_work_estimate(N2, Nu, l), world, k) for k in range(world)]
+        for rank, idx, own, g, order in got:
+            np.testing.assert_array_equal(idx, owners[rank])
+            assert own == [o.tolist() for o in owners]
+        # the keyed deal is not the strided one here (it is the point of the test)
+        assert not np.array_equal(owners[0][owners[0] < len(N2)], np.arange(0, len(N2), 2))
+    else:
+        N2, Nu, d, l = _c4_grid()
+        sims = _c4_costs(N2, Nu, d, l).reshape(len(N2), C4_DRAWS, 2)
+        ref, w = sims.max(axis=1), np.ones(2)
+        assert np.all(sims.max(axis=1) > sims.min(axis=1))   # the draws differ: amax selects
+    C = len(N2)
+    per = -(-C // world)
+    ref_order = np.argsort(ref @ w, kind="stable")
+    for rank, idx, own, g, order in got:
+        assert g.shape == (world * per, ref.shape[1])
+        np.testing.assert_array_equal(g[:C], ref)          # bit-identical gathered records
+        assert np.all(np.isnan(g[C:]))                     # sentinel padding
+        np.testing.assert_array_equal(order, ref_order)    # identical ranking on every rank
+    np.testing.assert_array_equal(got[0][4], got[1][4])

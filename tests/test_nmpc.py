@@ -135,6 +135,41 @@ def test_nmpc_scenario_errors(built):
         nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 31, 17)
     with pytest.raises(MpctError, match="u_min"):
         nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMAX, nmpc.VDV_UMIN, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 31, 15)
+    with pytest.raises(MpctError, match="64 KiB"):
+        nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 400, 16)
+
+
+def test_nmpc_oracle_returned_iterate_drift():
+    """the controller returns the converged iterate v (round 4), not clip(v + d) (rounds
+    1-3).  Which one nlmpcmove returns is unpinned; the two conventions' closed loops stay within
+    5 SQP_TOL of each MV's ScaleFactor at every step and 1e-6 relative on J1 (measured on these
+    candidates: 2.3e-8 s_u and 7.3e-7 at most)."""
+    import oracle.nmpc_vdv as nv
+    from mpct.nmpc import nmpc_candidate_grid, steady_state, vandevusse_signals
+
+    r, yref = vandevusse_signals(steady_state())
+    N, Nu, d, lam = nmpc_candidate_grid(64)
+    for k in (0, 2, 3):
+        a = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], open_loop=False)
+        b = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], open_loop=False, return_step=True)
+        assert np.max(np.abs(a.u - b.u) / nv.SU[:, None]) <= 5 * nv.SQP_TOL, k
+        np.testing.assert_allclose(((a.y - yref) ** 2).sum(1), ((b.y - yref) ** 2).sum(1), rtol=COST_RTOL)
+
+
+def test_nmpc_long_horizon_point_buffers(built):
+    """the M <= 15 class's point buffers (four, two or one per simulation) are sized so
+    that every (N, Nu) of a long-horizon scenario with nu * nu_max > 15 fits 64 KiB: nu = 2,
+    nu_max = 8, n_max = 127 (M = 14 needed ~101 KB with two buffers) and n_max = 80, nu_max = 7
+    (refused at ~67 KB before)."""
+    from mpct import nmpc
+
+    x0 = nmpc.steady_state()
+    r, yref = nmpc.vandevusse_signals(x0)
+    for n_max, nu_max in ((127, 8), (80, 7)):
+        sc = nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref,
+                               n_max, nu_max)
+        lds = [sc.lds_bytes(N, Nu) for N in range(1, n_max + 1) for Nu in range(1, nu_max + 1)]
+        assert max(lds) <= 64 * 1024, (n_max, nu_max, max(lds))
 
 
 @pytest.fixture(scope="module")
@@ -176,6 +211,31 @@ def test_nmpc_gpu_matches_oracle(gpu):
             xr = np.abs(o.uopt[:, :1]) / du
         xr[~np.isfinite(xr)] = 0.0
         np.testing.assert_allclose(res.Jnu[k], (xr ** 2).sum(1), rtol=COST_RTOL)
+
+
+@pytest.mark.gpu
+def test_nmpc_gpu_long_horizon_point_buffers(gpu):
+    """long horizons in the M <= 15 class (nu = 2, nu_max = 8, n_max = 127) run with
+    one or two point buffers instead of four (nm_groups); N = 127, Nu = 7 (M = 14, one buffer)
+    and N = 70, Nu = 7 (two) equal the oracle's loop, and no slot is left unsimulated."""
+    import oracle.nmpc_vdv as nv
+    from mpct import nmpc
+    from mpct.engine import eval_batch
+
+    x0 = nmpc.steady_state()
+    r, yref = nmpc.vandevusse_signals(x0)
+    sc = nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 127, 8)
+    N = np.array([127, 70, 31], np.int32)
+    Nu = np.array([7, 7, 8], np.int32)
+    d = np.array([[1.0, 0.5], [0.7, 1.0], [1.0, 1.0]])
+    lam = np.array([[0.1, 0.1], [0.05, 0.2], [0.1, 0.1]])
+    res = eval_batch(sc, N, Nu, d, lam, r[None], want_traj=True)
+    assert np.all(res.status == 0), res.status
+    for k in range(2):
+        o = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k], open_loop=False)
+        for a, b in ((res.y[k], o.y), (res.u[k], o.u)):
+            assert _trel(a, b) < TRAJ_RTOL, (k, _trel(a, b))
+        np.testing.assert_allclose(res.J1[k], ((o.y - yref) ** 2).sum(1), rtol=COST_RTOL)
 
 
 @pytest.mark.gpu

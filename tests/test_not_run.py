@@ -1,0 +1,124 @@
+"""Unclaimed simulation slots.  Every eval path splits a batch into class
+launches (QP size x LDS tier) that each span the whole batch, and a simulation runs only in the
+launch whose class holds it.  A slot that no launch claims used to return whatever the output
+buffer held, with status 0 (the r04g NMPC fault: some (M, N) pairs fell into no LDS tier).  Now
+every slot is prefilled with MPCT_ST_NOT_RUN and NaN costs before the class launches
+(work_order.hip prefill_results), and only the launch that simulates a slot overwrites its record.
+The reference treats a failed sim as an error, never as a value (VNS2.m:151-163, GAM_fun.m:82-84).
+
+GPU: the full config-3 and config-5 grids and a mixed-horizon Shell 3x3 batch leave no NOT_RUN
+bit; a planted fault (MPCT_DIAG_DROP_LAUNCH: one class launch not issued) comes back NOT_RUN with
+NaN costs on exactly the dropped class's slots, and objectives.failed() rejects them."""
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_not_run_status_is_fatal_and_in_the_header():
+    import re
+
+    from mpct import _lib
+    from mpct.objectives import FATAL_STATUS, failed
+
+    hdr = open(os.path.join(ROOT, "include", "mpct.h")).read()
+    assert int(re.search(r"#define MPCT_ST_NOT_RUN (\d+)", hdr).group(1)) == _lib.ST_NOT_RUN == 128
+    assert FATAL_STATUS & _lib.ST_NOT_RUN
+    assert failed([0, 128, 1]).tolist() == [False, True, False]
+    # the MATLAB drop-ins raise mpct:sim / mpct:nlmpc on exactly the Python host's fatal bits
+    for f in ("closedloop_toolbox.m", "closedloop_toolbox_nmpc.m", "closedloop_gpc_batch.m"):
+        m = re.search(r"bitand\(status, ([0-9 +]+)\)", open(os.path.join(ROOT, "matlab", f)).read())
+        assert sum(int(x) for x in m.group(1).split("+")) == FATAL_STATUS, f
+    src = open(os.path.join(ROOT, "model-predictive-control-tuning_amd", "csrc", "work_order.hip")).read()
+    assert "prefill_kernel" in src
+    # every launcher prefills before its class launches fork
+    for f, call in (("gpc_kernel.hip", "prefill_results(lo"), ("mdband_kernel.hip", "prefill_results(out"),
+                    ("nmpc_kernel.hip", "prefill_results(out")):
+        s = open(os.path.join(ROOT, "model-predictive-control-tuning_amd", "csrc", f)).read()
+        assert s.index(call) < s.index("FanScope fs("), f
+
+
+@pytest.fixture(scope="module")
+def gpu(built, has_gpu):
+    if not has_gpu:
+        pytest.skip("no GPU")
+    return True
+
+
+def _mixed_shell3x3():
+    """Shell 3x3 with nu_max = 15: every QP-size class (16 / 32 / 64) of the general kernel, the
+    small-plant kernel's class, padding and bad horizons, three VNS reference sets."""
+    from mpct.scenarios import shell3x3, vns_step_refs
+
+    rng = np.random.default_rng(11)
+    C = 300
+    N2 = rng.integers(16, 41, size=C).astype(np.int32)
+    Nu = np.minimum(rng.integers(1, 16, size=C), N2).astype(np.int32)
+    N2[:3], Nu[:3] = (0, 41, 5), (2, 2, 9)  # skipped, N2 > n2_max, Nu > N2
+    d = 10.0 ** rng.uniform(-3, 0, size=(C, 3))
+    l = 10.0 ** rng.uniform(-3, -1, size=(C, 3))
+    sc, r, yref = shell3x3(n2_max=40, nu_max=15, nit=120)
+    return sc, N2, Nu, d, l, r, vns_step_refs(3, 120)
+
+
+@pytest.mark.gpu
+def test_no_slot_left_unsimulated(gpu):
+    """Config 3 (65,536 band-mode candidates, every LDS tier), config 5 (4,096 NMPC candidates, both
+    QP-size classes, with and without the open-loop leg) and a mixed-horizon Shell 3x3 batch (cost
+    only and with the open-loop leg): no NOT_RUN bit anywhere."""
+    from mpct import _lib
+    from mpct.engine import eval_batch
+    from mpct.nmpc import nmpc_candidate_grid, vandevusse
+    from mpct.scenarios import config3_grid, shell7x5
+
+    sc3, r3, v3, _ = shell7x5(n2_max=127, nu_max=15)
+    N2, Nu, D, L = config3_grid(1024)
+    res = eval_batch(sc3, N2, Nu, D, L, r3[None], v=v3[None])
+    assert not np.any(res.status & _lib.ST_NOT_RUN), np.flatnonzero(res.status & _lib.ST_NOT_RUN)[:8]
+    assert np.all(res.status == 0)
+    sc5, r5, _ = vandevusse()
+    N, Nu5, d5, l5 = nmpc_candidate_grid(4096)
+    for ol in (False, True):
+        res = eval_batch(sc5, N, Nu5, d5, l5, r5[None], open_loop=ol)
+        assert not np.any(res.status & _lib.ST_NOT_RUN), (ol, np.flatnonzero(res.status & _lib.ST_NOT_RUN)[:8])
+    sc, N2, Nu, d, l, r, refs = _mixed_shell3x3()
+    for rr, ol in ((r[None], False), (refs, False), (refs, True)):
+        res = eval_batch(sc, N2, Nu, d, l, rr, open_loop=ol)
+        st = res.status.reshape(N2.size, -1)
+        assert not np.any(st & _lib.ST_NOT_RUN), (ol, np.flatnonzero(np.any(st & _lib.ST_NOT_RUN, axis=1))[:8])
+        assert np.all(st[0] == 8) and np.all(st[1] == 16) and np.all(st[2] == 16)
+
+
+@pytest.mark.gpu
+def test_dropped_class_launch_reports_not_run(gpu, monkeypatch):
+    """A planted dispatch fault: with MPCT_DIAG_DROP_LAUNCH=k the k-th class launch of the batch is
+    not issued.  Exactly the slots of its class come back NOT_RUN with NaN costs and 0 iterations;
+    every other slot equals the fault-free run bit for bit; failed() rejects the dropped ones."""
+    from mpct import _lib
+    from mpct.engine import eval_batch
+    from mpct.objectives import failed
+
+    sc, N2, Nu, d, l, r, refs = _mixed_shell3x3()
+    M = 3 * Nu.astype(int)
+    valid = (N2 > 0) & (N2 <= 40) & (Nu <= N2)
+    base = eval_batch(sc, N2, Nu, d, l, refs)
+    assert not np.any(base.status & _lib.ST_NOT_RUN)
+    # the general kernel's class launches in order: M <= 16 (k = 0), 32 (k = 1), 64 (k = 2); launch 0
+    # also writes the padding / bad-horizon statuses
+    for k, (lo, hi) in ((1, (16, 32)), (2, (32, 64))):
+        monkeypatch.setenv("MPCT_DIAG_DROP_LAUNCH", str(k))
+        res = eval_batch(sc, N2, Nu, d, l, refs)
+        monkeypatch.delenv("MPCT_DIAG_DROP_LAUNCH")
+        dropped = valid & (M > lo) & (M <= hi)
+        assert dropped.sum() > 10
+        st = res.status.reshape(N2.size, -1)
+        assert np.all(st[dropped] == _lib.ST_NOT_RUN), np.unique(st[dropped])
+        assert np.all(failed(st[dropped]))
+        J1 = res.J1.reshape(N2.size, -1, 3)
+        assert np.all(np.isnan(J1[dropped]))
+        assert np.all(res.qp_iters.reshape(N2.size, -1)[dropped] == 0)
+        keep = ~dropped
+        np.testing.assert_array_equal(st[keep], base.status.reshape(N2.size, -1)[keep])
+        np.testing.assert_array_equal(J1[keep], base.J1.reshape(N2.size, -1, 3)[keep])
