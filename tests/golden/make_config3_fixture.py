@@ -10,7 +10,12 @@ restates closedloop_toolbox.m:36-100 for Shell7x5.m:98-196).
 
 Inputs: mpct.scenarios.config3_grid (N2 x Nu x 1024 lambda draws, seed 20250307, delta = 0),
 r = 0, v = the measured disturbance step, nit = 200, GAM mode (no open-loop leg).
-Run:  python tests/golden/make_config3_fixture.py [--threads 8]   (≈15 min on 8 cores)."""
+Run:  python tests/golden/make_config3_fixture.py [--threads 8]   (≈15 min on 8 cores).
+
+--warm writes tests/golden/config3_cband_warm.npz instead: the same grid scored by the C
+restatement's second, equally valid QP path (each step's dual method warm-started from the previous
+step's final active set, cband.c cb_scen.qp_warm; F_full, st_full).  Its distance to the cold
+fixture is the C-vs-C floor of the config-3 parity (tools/config3_floor.py)."""
 import argparse
 import os
 import sys
@@ -26,15 +31,17 @@ from oracle.cband import CBand  # noqa: E402
 from oracle.scenarios import shell7x5  # noqa: E402
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config3_cband.npz")
+OUT_WARM = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config3_cband_warm.npz")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=2048)
+    ap.add_argument("--warm", action="store_true")
     a = ap.parse_args()
     sc, r, v, yref, fx = shell7x5()
-    cb = CBand(sc, 200, yref)
+    cb = CBand(sc, 200, yref, warm=a.warm)
     N2, Nu, D, L = config3_grid(1024)
     C = N2.size
     J1 = np.zeros((C, 7))
@@ -48,6 +55,10 @@ def main():
         o = cb.eval(N2[idx], Nu[idx], D[idx], L[idx], r[None], v[None], threads=a.threads)
         J1[idx], st[idx], it[idx] = o["J1"], o["status"], o["qp_iters"]
         print("%d / %d  %.0f s" % (k + idx.size, C, time.time() - t0), flush=True)
+    if a.warm:
+        np.savez_compressed(OUT_WARM, F_full=J1 @ SHELL7_W, st_full=st.astype(np.int8))
+        print("wrote", OUT_WARM, "status != 0:", int(np.sum(st != 0)))
+        return
     s = config3_stratified(128)
     np.savez_compressed(OUT, J1_strat=J1[s], it_strat=it[s], F_full=J1 @ SHELL7_W, st_full=st.astype(np.int8))
     print("wrote", OUT, "status != 0:", int(np.sum(st != 0)))

@@ -440,34 +440,34 @@ def test_rank_stats_small():
 
 @pytest.mark.gpu
 def test_band_config3_grid_costs_against_c_port(gpu):
-    """Config-3 cost parity over the grid: the whole 65,536-candidate grid on
-    the device against the C restatement's committed costs (tests/golden/config3_cband.npz,
+    """Config-3 cost parity over the grid: the whole 65,536-candidate
+    grid on the device against the C restatement's committed costs (tests/golden/config3_cband.npz,
     oracle/cband.c):
     * every simulation succeeds, and the ranking under SHELL7_W (Shell7x5.m:202, what the tuner
-      consumes) is identical over its first 3,000 places (measured: the first 3,566, the first
-      difference a pair of candidates 2e-6 apart in F; profiles/r04zr_config3_ranking.json);
-    * at most 1.45 % of the candidates' Pareto-weighted costs F = J1 @ SHELL7_W differ by more than
-      1e-6 relative (measured 1.34 %, profiles/r04x_config3_rebuild_interval_sweep.jsonl), and at
-      most 8.5 % of the stratified sample's per-output J1 (measured 7.80 %);
-    * the full-grid ranking under F (rank_stats): candidates displaced, the largest displacement,
-      discordant pairs and discordant pairs the 1e-6 bar separates are bounded just above their
-      measured values (DESIGN §3), so a regression that widens the divergence fails;
-    * 24 divergent candidates of the stratified sample (J1 beyond 1e-6 on some output) take, at
-      every one of their 200 steps, the oracle's optimal move at the state they reached (1e-6 of
-      the largest move) -- or, at the first four steps of each where the moves differ, a move
-      that attains the oracle QP's optimal cost to 1e-6 relative (oracle QP with the first moves
-      pinned to the device's, toolbox_band.pinned_gap; plus 1e-12 of the QP cost at the
-      trajectory's largest move, the squared counterpart of the moves' 1e-6 of the largest move).  Those are steps where the soft-band slack dominates the cost
-      and the optimum is flat along the moves."""
+      consumes) is identical over its first 3,000 places (measured: the first 3,566);
+    * EVERY divergent candidate is certified (tools/config3_certify.py, profiles/r05_config3_certify.json):
+      a candidate whose F = J1 @ SHELL7_W, or (stratified sample) any per-output J1, differs by more
+      than 1e-6 is replayed by the C restatement at the states the device reached (cband_replay_gap):
+      at every step its move equals the oracle's to 1e-6 of the largest move, or it attains the oracle
+      QP's optimal cost (QP with the first moves pinned to the device's; 1e-6 of the QP cost plus
+      1e-12 of the cost at the trajectory's largest move, the squared counterpart of the moves' 1e-6).
+      Measured: 1,392 divergent, 888 equal at every step, 504 flat at 1,295 steps, none uncertified;
+    * against the floor: the C restatement's second, equally valid QP path (warm-started
+      dual method, tests/golden/config3_cband_warm.npz) differs from its cold path by more than 1e-6
+      on 1.00 % of F.  The device is no farther from that second C path than the two C paths are from
+      each other (measured 0.89 %; bound: the floor + 0.2 %), and 1.34 % from the cold path (bound
+      1.45 %, the round-4 bound: the device's path is warm-started like the second C path);
+    * the full-grid ranking statistics against the cold fixture stay within CONFIG3_RANK_BOUNDS."""
     import os
 
     from mpct.engine import eval_batch
     from mpct.scenarios import SHELL7_W, config3_grid, config3_stratified, shell7x5
     from oracle.cband import CBand
     from oracle.scenarios import shell7x5 as o_shell7x5
-    from oracle.toolbox_band import pinned_gap
 
-    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config3_cband.npz"))
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    d = np.load(os.path.join(g, "config3_cband.npz"))
+    dw = np.load(os.path.join(g, "config3_cband_warm.npz"))
     sc, r, v, yref = shell7x5(n2_max=127, nu_max=15)
     N2, Nu, D, L = config3_grid(1024)
     res = eval_batch(sc, N2, Nu, D, L, r[None], v=v[None])
@@ -476,35 +476,40 @@ def test_band_config3_grid_costs_against_c_port(gpu):
     o_dev, o_ref = np.argsort(F, kind="stable"), np.argsort(d["F_full"], kind="stable")
     first = np.nonzero(o_dev != o_ref)[0]
     prefix = int(first[0]) if first.size else F.size
-    print("config3: identical ranking prefix %d" % prefix)
-    assert prefix >= 3000, prefix
     relF = np.abs(F - d["F_full"]) / np.abs(d["F_full"])
+    relW = np.abs(F - dw["F_full"]) / np.abs(dw["F_full"])
+    floor = float(np.mean(np.abs(dw["F_full"] - d["F_full"]) / np.abs(d["F_full"]) > COST_RTOL))
     s = config3_stratified(128)
     relJ = np.max(np.abs(res.J1[s] - d["J1_strat"]) / np.abs(d["J1_strat"]), axis=1)
     rs = rank_stats(F, d["F_full"])
-    print("config3: F beyond 1e-6: %.4f of the grid (median %.1e); J1 beyond 1e-6: %.4f of the sample; "
-          "ranking %s" % (np.mean(relF > COST_RTOL), np.median(relF), np.mean(relJ > COST_RTOL), rs))
+    print("config3: identical ranking prefix %d; F beyond 1e-6: %.4f of the grid against the cold C path, %.4f "
+          "against the warm C path (floor: C warm vs cold %.4f); J1 beyond 1e-6: %.4f of the sample; ranking %s"
+          % (prefix, np.mean(relF > COST_RTOL), np.mean(relW > COST_RTOL), floor, np.mean(relJ > COST_RTOL), rs))
+    assert prefix >= 3000, prefix
     assert np.mean(relF > COST_RTOL) <= 0.0145
+    assert np.mean(relW > COST_RTOL) <= floor + 0.002
     assert np.mean(relJ > COST_RTOL) <= 0.085
     for k, bound in CONFIG3_RANK_BOUNDS.items():
         assert rs[k] <= bound, (k, rs[k], bound)
-    div = s[relJ > COST_RTOL]
-    pick = div[np.linspace(0, div.size - 1, min(24, div.size)).astype(int)] if div.size else div
-    if pick.size:
-        osc, orr, ov, oyref, fx = o_shell7x5()
-        g = eval_batch(sc, N2[pick], Nu[pick], D[pick], L[pick], r[None], v=v[None], want_traj=True)
-        du_o, du_a, st = CBand(osc, 200, oyref).replay(N2[pick], Nu[pick], D[pick], L[pick], orr, ov, g.u,
-                                                     T=200, threads=16)
-        assert np.all(st == 0)
-        for k, c in enumerate(pick):
-            err = np.abs(du_a[k] - du_o[k]).max(axis=0) / np.abs(du_o[k]).max()
-            bad = np.nonzero(err > REPLAY_RTOL)[0][:4]
-            if not bad.size:
-                continue
-            args = (osc, orr, ov, int(N2[c]), int(Nu[c]), D[c], L[c], g.u[k])
-            # the move tolerance is relative to the trajectory's largest move, so the cost one is
-            # relative to the QP cost at that step as well (squared: 1e-6 of a move ~ 1e-12 of J)
-            J_scale = pinned_gap(*args, int(np.abs(du_a[k]).max(axis=0).argmax()))[0]
-            for t in bad:
-                J0, J1, _ = pinned_gap(*args, int(t))
-                assert J1 - J0 <= COST_RTOL * J0 + 1e-12 * J_scale, (int(c), int(t), J0, J1, J_scale)
+    # certify every divergent candidate by the C replay at the device's own states
+    div = np.union1d(np.nonzero(relF > COST_RTOL)[0], s[relJ > COST_RTOL])
+    gt = eval_batch(sc, N2[div], Nu[div], D[div], L[div], r[None], v=v[None], want_traj=True)
+    osc, orr, ov, oyref, fx = o_shell7x5()
+    du_o, du_a, J0, J1, st = CBand(osc, 200, oyref).replay_gap(N2[div], Nu[div], D[div], L[div], orr, ov, gt.u,
+                                                               threads=16)
+    assert np.all(st == 0)
+    bad, flat = [], 0
+    for k, c in enumerate(div):
+        err = np.abs(du_a[k] - du_o[k]).max(axis=0) / np.abs(du_o[k]).max()
+        ts = np.nonzero(err > REPLAY_RTOL)[0]
+        if not ts.size:
+            continue
+        Js = J0[k, int(np.abs(du_a[k]).max(axis=0).argmax())]
+        gap = J1[k, ts] - J0[k, ts]
+        ok = np.isfinite(gap) & (gap <= COST_RTOL * J0[k, ts] + 1e-12 * Js)
+        flat += 1
+        if not np.all(ok):
+            bad.append((int(c), ts[~ok][:4].tolist()))
+    print("config3: %d divergent candidates, %d with moves equal to the oracle's at every step, %d flat"
+          % (div.size, div.size - flat, flat))
+    assert not bad, bad[:8]

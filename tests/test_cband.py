@@ -128,3 +128,42 @@ def test_pinned_gap_judges_moves_by_cost(shell):
     Uw[0, 20:] += 0.05 * abs(Uw[0, 20] - Uw[0, 19])
     J0, J1, _ = pinned_gap(wsc, wr, wv, 12, 3, d, lw, Uw, 20)
     assert J1 - J0 > 1e-6 * J0
+
+
+def test_cband_replay_gap_equals_numpy_pinned_gap(shell):
+    """cband_replay_gap (the C certification of config-3 divergences, tools/config3_certify.py)
+    equals toolbox_band.pinned_gap: the free and the pinned QP objectives at the states a perturbed
+    trajectory reached, and on the C port's own trajectory the moves replay exactly."""
+    from oracle.toolbox_band import pinned_gap
+
+    sc, r, v, yref, fx, cb = shell
+    N2, Nu, lm = 16, 3, np.array([0.1, 0.03, 2.0])
+    o = cb.eval([N2], [Nu], np.zeros((1, 7)), lm[None], r[None], v[None], want_traj=True)
+    U = o["u"][0]
+    du_o, du_a, J0, J1, st = cb.replay_gap([N2], [Nu], np.zeros((1, 7)), lm[None], r, v, U[None], threads=2)
+    assert st[0] == 0
+    assert np.max(np.abs(du_o - du_a)) <= 1e-12 * np.abs(du_a).max()
+    Up = U.copy()
+    Up[0, 30:] += 1e-4
+    du_o, du_a, J0, J1, st = cb.replay_gap([N2], [Nu], np.zeros((1, 7)), lm[None], r, v, Up[None], threads=2)
+    for t in (25, 30, 60):
+        a, b, _ = pinned_gap(sc, r, v, N2, Nu, np.zeros(7), lm, Up, t)
+        np.testing.assert_allclose([J0[0, t], J1[0, t]], [a, b], rtol=1e-12)
+
+
+def test_cband_warm_path_fixture(shell):
+    """The C restatement's second QP path (warm-started dual method, cb_scen.qp_warm) reproduces its
+    committed grid costs (tests/golden/config3_cband_warm.npz, the C-vs-C floor of DESIGN §3) on a
+    sample of the grid, and differs from the cold path's fixture on ~1 % of F beyond 1e-6."""
+    from mpct.scenarios import SHELL7_W, config3_grid
+    from oracle.cband import CBand
+
+    sc, r, v, yref, fx, cb = shell
+    dw = np.load(os.path.join(os.path.dirname(__file__), "golden", "config3_cband_warm.npz"))
+    d = np.load(FIXTURE)
+    N2, Nu, D, L = config3_grid(1024)
+    idx = np.arange(0, N2.size, 4099)[:16]
+    o = CBand(sc, 200, yref, warm=True).eval(N2[idx], Nu[idx], D[idx], L[idx], r[None], v[None], threads=4)
+    np.testing.assert_allclose(o["J1"] @ SHELL7_W, dw["F_full"][idx], rtol=1e-12)
+    floor = np.mean(np.abs(dw["F_full"] - d["F_full"]) / np.abs(d["F_full"]) > 1e-6)
+    assert 0.005 < floor < 0.015, floor

@@ -1,0 +1,111 @@
+"""Latency roofline of the metric kernel: the dependent chain of one closed-loop
+step of gpc_small_kernel, priced with the primitive latencies measured on the GPU
+(tools/latency_probe.hip -> profiles/r05_latency_probe.json), against the cycles the heaviest
+simulations actually spend (the -DMPCT_PROFILE build's s_memtime section stamps and section
+counts, tools/kprof.py with MPCT_PROF_OUT).
+
+Each section of the step (gpc_small.hip, gpc_qp16.h; the sections of mpct_dev.h PROF_*) is a chain
+of primitives whose results the next one waits for; work off that chain (the A rows' loads, the
+other three accumulators of a FOR4, the J1 cost) is not counted.  chain(section) = sum over its
+primitives of their measured dependent latency; model = sum over sections of chain x executions;
+latency_frac = model / measured.  1.0 would mean the kernel runs at the speed of its own dependency
+chain with nothing else in the way (issue contention of the SIMD's other waves, instruction issue
+of the off-chain work, LDS bank conflicts, waits the compiler's schedule adds).
+
+Usage: python tools/latency_model.py PROBE.json PROF.bin [--out FILE]
+  PROF.bin: the per-simulation section words of the profiled heavy batch (MPCT_PROF_OUT)."""
+import argparse
+import json
+import sys
+
+import numpy as np
+
+SECTIONS = ["prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update", "open_loop",
+            "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations"]
+
+# The chain of each section, per execution, as primitive -> count.  Read off gpc_small.hip's step
+# loop and gpc_qp16.h (file:line in the comments); names are tools/latency_probe.hip's probes.
+CHAINS = {
+    # ring store of the last step's u update -> lds_sync -> the term's ring read -> coef * hv ->
+    # v_permlane16/32 row sum over the four term rows -> two quad DPP stages (gpc_small.hip:164-169)
+    "plant": {"lds_handoff": 1, "fma_f64": 1, "row4_sum_permlane": 1, "dpp_stage_f64": 2},
+    # n1 = y - y(t-1), n2 = n1 - o1, n3 = n2 - o2, stored, lds_sync, read by the product (:173-195)
+    "y_update": {"add_f64": 3, "lds_handoff": 1},
+    # 6 dependent FMAs per accumulator over quarter 0's 12 columns, the pair add, the row4 sum (:198-221)
+    "unconstrained": {"fma_f64": 6, "add_f64": 1, "row4_sum_permlane": 1},
+    # the QP entry on a feasible x_u: box slacks (block prefix over the MV's moves), the four
+    # slacks' min, the ballot (gpc_qp16.h:336-369); u(t-1) of the row's MV arrives off the chain
+    "qp(rest)": {"block_prefix16_nu5": 1, "add_f64": 4, "ballot_branch": 1},
+    # the first move by ds_bpermute from the QP's register result, u = u(t-1) + du, ring store (:234-247)
+    "u_update": {"shfl_bpermute": 1, "add_f64": 1},
+    # most violated inactive constraint: slacks at x, the min over the lane's four kinds, the packed-
+    # key DPP argmin, the winner's value by readlane, the branch (gpc_qp16.h:445-461)
+    "qp.check": {"block_prefix16_nu5": 1, "add_f64": 4, "qargmin16_key": 1, "uniform_branch": 1},
+    # d = J'n_p (row16 DPP sum, four chains side by side), the products' d^2 FOR4 chain and one
+    # permlane row4 sum (the five run side by side) (gpc_qp16.h:192-225, :478-484)
+    "qp.d+z": {"row_sum16": 1, "mul_f64": 2, "add_f64": 4, "row4_sum_permlane": 1},
+    # ratio test: qp_div (rcp + Newton), the packed-key argmin, t2 beside it, two uniform branches,
+    # x += t z (gpc_qp16.h:485-506)
+    "qp.r+t1": {"rcp_nr": 1, "mul_f64": 1, "qargmin16_key": 1, "uniform_branch": 2, "fma_f64": 1},
+    # add: d_q by readlane, |d(q:)| by rsq, 2/v'v by rcp, the J column update, B / R_A columns to LDS,
+    # lds_sync before the next read (gpc_qp16.h:229-263)
+    "qp.add": {"bcast_readlane": 1, "rsq_nr": 1, "fma_f64": 2, "rcp_nr": 1, "mul_f64": 1, "lds_handoff": 1},
+    # drop: readlane of the id, R_A / B column shifts and the Givens sweep through LDS (per rotation:
+    # two entries read, rsq, the RMW of R_A and B, lds_sync), B's row shift (gpc_qp16.h:268-322);
+    # priced per drop with one rotation (the counted rotations add per rotation below)
+    "qp.drop": {"bcast_readlane": 1, "lds_handoff": 3, "dpp_stage_f64": 1},
+    # warm start: the slacks' gather by ds_bpermute, w = B'c (row16 DPP), x = x_u + J w and
+    # lambda = B w (FOR4 chains + permlane row4 sums), the multipliers' packed-key argmin, the
+    # branch (gpc_qp16.h:396-440); per pass of its loop
+    "qp.warm": {"shfl_bpermute": 1, "mul_f64": 1, "row_sum16": 1, "fma_f64": 4, "row4_sum_permlane": 1,
+                "add_f64": 1, "qargmin16_key": 1, "uniform_branch": 1},
+}
+# one Givens rotation of the drop: entries read, a^2 + b^2, rsq + Newton, cs / sn, the RMW of R_A's
+# two rows, lds_sync (gpc_qp16.h:289-310)
+ROTATION = {"lds_handoff": 1, "fma_f64": 1, "rsq_nr": 1, "mul_f64": 1}
+
+
+def chain_cycles(chain, lat):
+    return sum(n * lat[k] for k, n in chain.items())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("probe")
+    ap.add_argument("prof")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    lat = json.load(open(a.probe))
+    raw = np.fromfile(a.prof, dtype=np.uint64)
+    width = len(SECTIONS) if raw.size % len(SECTIONS) == 0 and raw.size % 13 else 13  # pre-r05 dumps: 13
+    raw = raw.reshape(-1, width)
+    cyc = (raw & np.uint64((1 << 48) - 1)).astype(np.float64)
+    cnt = (raw >> np.uint64(48)).astype(np.float64)
+    S = raw.shape[0]
+    rows = {}
+    model = measured = 0.0
+    for k, name in enumerate(SECTIONS):
+        if name not in CHAINS:
+            continue
+        per = chain_cycles(CHAINS[name], lat)
+        n = cnt[:, k].mean()
+        m = cyc[:, k].mean()
+        mod = per * n
+        if name == "qp.drop" and width > 13:  # plus the counted Givens rotations of every drop
+            mod += chain_cycles(ROTATION, lat) * cnt[:, SECTIONS.index("qp.rotations")].mean()
+        rows[name] = dict(executions=round(n, 1), chain_cycles=round(per, 1), model=round(mod),
+                          measured=round(m), frac=round(mod / m, 3) if m else None)
+        model += mod
+        measured += m
+    rep = dict(simulations=int(S), probe=a.probe, model_cycles=round(model), measured_cycles=round(measured),
+               latency_frac=round(model / measured, 3), sections=rows,
+               note="measured excludes the prologue (once per simulation); cycles per simulation, mean over "
+                    "the batch; stamps add ~11 % to the measured side (MI355X_MICROARCH.md)")
+    print(json.dumps(rep, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rep, f, indent=1)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
