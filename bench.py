@@ -205,6 +205,27 @@ def pmc_traffic(C, n2, nu):
             pj.get("fp64_counter"))
 
 
+def latency_roofline():
+    """roofline.latency_frac from the committed latency model (profiles/latency_latest.json, written by
+    tools/latency_model.py): the dependent chain of the heaviest 256 simulations priced with the
+    measured primitive latencies (tools/latency_probe.hip), over their measured time -- accepted only
+    when the model was fitted to this very library (same sha256).  Returns (frac | None, note)."""
+    p = os.path.join(ROOT, "profiles", "latency_latest.json")
+    if not os.path.exists(p):
+        return None, "no latency model committed"
+    try:
+        with open(p) as f:
+            lj = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable profiles/latency_latest.json"
+    mine = lib_sha256()
+    if lj.get("lib_sha256") != mine:
+        return None, "latency model fitted to libmpct.so sha256 %s, this run loaded %s: not used" % (
+            str(lj.get("lib_sha256"))[:16], mine[:16])
+    return lj.get("latency_frac"), "%s (chain model of the heaviest 256, libmpct.so sha256 %s)" % (
+        lj.get("source", "profiles/latency_latest.json"), mine[:16])
+
+
 def cpu_model() -> str:
     """The host CPU's model name (report the baseline's cores and CPU model)."""
     try:
@@ -331,6 +352,7 @@ def main():
         return
 
     traffic, traffic_source, fp64c = pmc_traffic(C, args.n2, args.nu)
+    lat_frac, lat_source = latency_roofline()
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -393,6 +415,9 @@ def main():
                      # what the SIMDs issued, from the same sha-keyed PMC pass: every
                      # FP64 VALU wave-instruction at 64 lanes over the rocprof kernel time
                      "fp64_counter_tflops": fp64c.get("tflops") if fp64c else None,
+                     # dependent-chain model time / measured time of the heaviest 256 simulations
+                     # (tools/latency_model.py): how close the tail sits to its own chain
+                     "latency_frac": lat_frac, "latency_source": lat_source,
                      "bound_note": "FP64 vector ALU issue + per-step dependent latency (no MFMA on this path: "
                                    "DESIGN §6); peak = MI355X FP64 vector dense peak"},
         "cpu_baseline": cpu,

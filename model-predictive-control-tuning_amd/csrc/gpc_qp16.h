@@ -430,6 +430,9 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         int kd = i;
         qargmin<16>(lmin, kd, 0);
         if (!(lmin < 0.0)) break;
+#ifdef MPCT_PROFILE
+        pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
+#endif
         gi16_drop(S, F, sRA, M, kd, mark);
         {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
           const double cn = lane_next<16>(c);
@@ -509,6 +512,9 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         PSTAMP(PROF_QADD);
         break;
       }
+#ifdef MPCT_PROFILE
+      pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kdrop) * kProfCount;
+#endif
       gi16_drop(S, F, sRA, M, kdrop, mark);
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {

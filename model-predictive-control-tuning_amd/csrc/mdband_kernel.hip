@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "gi_core.h"
 #include "launch_fan.h"
 #include "mpct_dev.h"
@@ -50,6 +52,12 @@
 #define MPCT_BAND_RELTOL 1e-12
 #endif
 constexpr double kRelTol = MPCT_BAND_RELTOL;
+// the output rows' inverse norms |n o D|^-1 (the constraint choice and the termination test): float
+// (4 B per row side) or, MPCT_BAND_RN_F64, double as the oracle computes them
+#ifndef MPCT_BAND_RN_F64
+#define MPCT_BAND_RN_F64 0
+#endif
+typedef std::conditional_t<MPCT_BAND_RN_F64 != 0, double, float> rn_t;
 
 namespace mpct {
 
@@ -109,7 +117,7 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.uring = take(ncopy * nin * L.ur);
   L.tail = take(ne * L.ts);  // model entry tails of the window (mz_na - 1 entries each)
   L.sext = take(ne);            // model entry window extensions
-  L.rn = take(my * N2);         // output rows' inverse norms: 2 floats (upper, lower) per row
+  L.rn = take(my * N2 * (MPCT_BAND_RN_F64 ? 2 : 1));  // output rows' inverse norms: 2 rn_t (upper, lower) per row
   L.plb = take(ne * sc.pl_maxbc);  // compact: taps from the first nonzero one
   L.pla = take(ne * sc.pl_maxa);
   L.mzb = take(ne * sc.mz_maxbc);
@@ -321,7 +329,7 @@ __global__ void __launch_bounds__(64, 1)
   // Box rows of lane m: kinds 0/1 (n = e_m), the cumulative kinds 2/3 (n = e_j0 + .. + e_m), eps >= 0
   // on lane M; output rows q = 2 g + side (upper, lower) from a float table (a selection weight only)
   double ib01 = 0.0, ib23 = 0.0;
-  const float* srn = reinterpret_cast<const float*>(lds + L.rn);
+  const rn_t* srn = reinterpret_cast<const rn_t*>(lds + L.rn);
   {
     const double d2 = row ? snv[lane] : 0.0;
     const double pre = block_prefix<MAXM>(d2, rcn.l, Nu, lane < M, sxc);
@@ -329,7 +337,7 @@ __global__ void __launch_bounds__(64, 1)
       ib01 = rsq_nr(d2);
       ib23 = lane < M ? rsq_nr(pre) : 0.0;
     }
-    float* wrn = reinterpret_cast<float*>(lds + L.rn);
+    rn_t* wrn = reinterpret_cast<rn_t*>(lds + L.rn);
     for (int g = lane; g < P; g += kWave) {
       const int i = g / N2, k = g - i * N2;
       const int lmax = min(Nu - 1, k + 1);
@@ -342,8 +350,8 @@ __global__ void __launch_bounds__(64, 1)
       // a zero normal (a hard bound inside the dead time) keeps norm 1, as the oracle's rn does
       // (toolbox_band.py band_qp, cband.c): its violation stays visible to the choice and the test
       const double nu2 = fma(vu * vu, de, a), nl2 = fma(vl * vl, de, a);
-      wrn[2 * g] = nu2 > 0.0 ? (float)rsq_nr(nu2) : 1.0f;
-      wrn[2 * g + 1] = nl2 > 0.0 ? (float)rsq_nr(nl2) : 1.0f;
+      wrn[2 * g] = nu2 > 0.0 ? (rn_t)rsq_nr(nu2) : (rn_t)1;
+      wrn[2 * g + 1] = nl2 > 0.0 ? (rn_t)rsq_nr(nl2) : (rn_t)1;
     }
     lds_sync();
   }

@@ -169,7 +169,8 @@ inline StageRow stage_row(const DevResult& o, int my, int nu) {
 
 // section ids of the diagnostic in-kernel stamps
 enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,
-       PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_QWARM, PROF_N = 13 };
+       PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_QWARM, PROF_QROT, PROF_N = 14 };
+// PROF_QROT: a count only (the drops' Givens rotations, gpc_qp16.h), no cycles
 // nmpc_kernel.hip's sections (same slots): the prediction with tangents and its streamed QR when
 // it starts an iteration, R^-1 and the unconstrained step, the QP, the Anderson candidate's
 // prediction, the full-step (alpha = 1) trial prediction, the shorter Armijo trials (tangent-free),

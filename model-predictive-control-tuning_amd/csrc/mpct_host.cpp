@@ -1062,20 +1062,30 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
     (void)hipStreamSynchronize(stream);
     (void)hipMemcpy(hp.data(), dprof, sizeof(unsigned long long) * S * PROF_N, hipMemcpyDeviceToHost);
     (void)hipFree(dprof);
-    double sum[PROF_N] = {0}, mx[PROF_N] = {0};
+    // low 48 bits: cycles, high 16: executions of the section (wave_ops.h PSTAMP)
+    const unsigned long long cmask = (1ull << 48) - 1;
+    double sum[PROF_N] = {0}, mx[PROF_N] = {0}, cnt[PROF_N] = {0};
     for (long long i = 0; i < S; ++i)
       for (int k = 0; k < PROF_N; ++k) {
-        sum[k] += (double)hp[i * PROF_N + k];
-        mx[k] = std::max(mx[k], (double)hp[i * PROF_N + k]);
+        sum[k] += (double)(hp[i * PROF_N + k] & cmask);
+        cnt[k] += (double)(hp[i * PROF_N + k] >> 48);
+        mx[k] = std::max(mx[k], (double)(hp[i * PROF_N + k] & cmask));
       }
+    if (const char* po = getenv("MPCT_PROF_OUT")) {  // per simulation, raw (tools/latency_model.py)
+      FILE* f = fopen(po, "wb");
+      if (f) {
+        fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+        fclose(f);
+      }
+    }
     const char* gpc_nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
-                                  "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm"};
+                                  "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations"};
     const char* nmpc_nm[PROF_N] = {"full_pass", "rinv+step", "qp", "anderson_pass", "ls_full_pass", "ls_trials",
-                                   "plant_rk4", "other", "-", "-", "-", "-", "-"};
+                                   "plant_rk4", "other", "-", "-", "-", "-", "-", "-"};
     const char** nm = s->nmpc ? nmpc_nm : gpc_nm;
-    fprintf(stderr, "[mpct profile] mean / max cycles per simulation over %lld sims\n", S);
+    fprintf(stderr, "[mpct profile] mean / max cycles and mean executions per simulation over %lld sims\n", S);
     for (int k = 0; k < PROF_N; ++k)
-      fprintf(stderr, "  %-14s %12.0f %12.0f\n", nm[k], sum[k] / (double)S, mx[k]);
+      fprintf(stderr, "  %-14s %12.0f %12.0f %10.1f\n", nm[k], sum[k] / (double)S, mx[k], cnt[k] / (double)S);
   }
 #endif
   return MPCT_OK;

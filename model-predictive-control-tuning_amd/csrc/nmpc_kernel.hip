@@ -33,7 +33,8 @@ namespace mpct {
 
 // lane groups of the multi-point prediction pass: the M <= 15 class runs up to four
 // points of one controller call at once, one per 16-lane DPP row (the pass is bound by the FP64
-// issue of one wave, not by its lanes); the M <= 32 class runs one
+// issue of one wave, not by its lanes); the M <= 32 class runs one (two points on 32-lane halves
+// were measured slower: the half broadcasts cost more than the shared passes save)
 template <int MAXM>
 constexpr int kNmRows = MAXM <= 16 ? 4 : 1;
 
@@ -776,20 +777,12 @@ __global__ void __launch_bounds__(64, 1)
 // ------------------------------------------------------------------------------------------
 // host-side launch
 #include <algorithm>
-#include <cstdlib>
 #include <string>
 
 #include "work_order.h"
 
 namespace mpct {
 
-// nmpc_rows.hip: the throughput mode's launches and its largest four-row LDS group
-int launch_nmpc_rows(const DevScenario& sc, long long C, int nref, const int* N, const int* Nu, const double* delta,
-                     const double* lambda, const double* r, const int* perm, const DevOpts& o,
-                     const DevResult& out, FanScope& fs, int& nl, bool& first, std::string* err);
-long long nmpc_rows_group_max(const DevScenario& sc);
-// simulations per batch from which the throughput mode runs (4096 fill 1024 waves: one per SIMD)
-constexpr long long kNmRowsMinS = 2048;
 
 // LDS tiers (KB) of the class launches.  One wave per SIMD (342 / 418 VGPRs), so at most four
 // workgroups per CU: the M <= 15 class sizes its point buffers to 40 KB (nm_groups), one tier;
@@ -853,29 +846,18 @@ int launch_nmpc(const DevScenario& sc, long long C, int nref, const int* N, cons
     *err = "n_max x nu*nu_max needs more than 64 KiB of LDS per simulation";
     return -4;
   }
-  // throughput mode (nmpc_rows.hip, four simulations per wave) for batches that fill the chip; the
-  // latency mode's speculation for small tuning batches (one simulation per wave).  MPCT_NMPC_ROWS=0
-  // / 1 forces either mode (tests compare them)
-  const long long S = C * nref;
-  bool rows = S >= kNmRowsMinS && nmpc_rows_group_max(sc) <= 160 * 1024;
-  if (const char* e = getenv("MPCT_NMPC_ROWS"))
-    if (*e) rows = atoi(e) != 0 && nmpc_rows_group_max(sc) <= 160 * 1024;
   const int* perm = nullptr;
   if (wo) {
-    const int rc0 = order_candidates(rows ? kOrderNmpcRows : kOrderNmpc, sc.my, sc.nu, C, N, Nu, delta, lambda, *wo,
-                                     &perm, stream, err);
+    const int rc0 = order_candidates(kOrderNmpc, sc.my, sc.nu, C, N, Nu, delta, lambda, *wo, &perm, stream, err);
     if (rc0) return rc0;
   }
-  int rc = prefill_results(out, S, sc.my, sc.nu, stream, err);
+  int rc = prefill_results(out, C * nref, sc.my, sc.nu, stream, err);
   if (rc) return rc;
   FanScope fs(fan, stream);  // forks after the sort: every class launch waits for the permutation
   int nl = 0;
   bool first = true;  // the first launch also writes the padding / bad-horizon statuses
   if (Mmax > 15) rc = launch_nmpc_t<32>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 15, first, err);
-  if (rc == 0) {
-    if (rows) rc = launch_nmpc_rows(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, first, err);
-    else rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);
-  }
+  if (rc == 0) rc = launch_nmpc_t<16>(sc, C, nref, N, Nu, delta, lambda, r, perm, o, out, fs, nl, 0, first, err);
   fs.join();
   if (perm) order_mark_used(*wo, stream);  // after the join: every class launch has read it
   return rc;

@@ -50,15 +50,27 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
+// DPP moves.  Controls whose every lane has a source within its row (quad_perm, row_mirror,
+// row_half_mirror, row_newbcast) use v_mov_b32_dpp without an `old` operand: the update_dpp(0, ..)
+// form makes the compiler zero a fresh register before every move (two v_mov_b32 per double,
+// ~60 per Goldfarb-Idnani step of the metric kernel).  The row shifts (row_shl / row_shr: lanes at
+// the row's edge have no source) keep old = 0; their callers never read those lanes.
+template <int CTRL>
+constexpr bool kDppAllLanes = CTRL < 0x100 || CTRL == 0x140 || CTRL == 0x141 || (CTRL >= 0x150 && CTRL <= 0x15F);
+template <int CTRL>
+__device__ __forceinline__ int dpp32(int v) {
+  if constexpr (kDppAllLanes<CTRL>) return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+  else return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = dpp32<CTRL>(__double2loint(v));
+  const int hi = dpp32<CTRL>(__double2hiint(v));
   return __hiloint2double(hi, lo);
 }
 template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return dpp32<CTRL>(v);
 }
 // DPP controls: quad_perm(1,0,3,2), quad_perm(2,3,0,1), row_half_mirror, row_mirror
 constexpr int kQx1 = 0xB1, kQx2 = 0x4E, kHalfMirror = 0x141, kMirror = 0x140;
@@ -93,17 +105,28 @@ __device__ __forceinline__ double row_bcast16(double v, int k) {
     default: return dppd<0x15F>(v);
   }
 }
-__device__ __forceinline__ void row_argmin_step(double& v, int& id, double pv, int pi) {
-  if (pv < v || (pv == v && pi < id)) {
-    v = pv;
-    id = pi;
-  }
+// min over the 16 lanes of each row, on every lane of the row (v_min_f64 on DPP-moved operands)
+__device__ __forceinline__ double row_min(double v) {
+  v = fmin(v, dppd<kQx1>(v));
+  v = fmin(v, dppd<kQx2>(v));
+  v = fmin(v, dppd<kHalfMirror>(v));
+  return fmin(v, dppd<kMirror>(v));
 }
+__device__ __forceinline__ int row_min_i(int v) {
+  v = min(v, dppi<kQx1>(v));
+  v = min(v, dppi<kQx2>(v));
+  v = min(v, dppi<kHalfMirror>(v));
+  return min(v, dppi<kMirror>(v));
+}
+// (v, id) -> the row's smallest v and the smallest id attaining it, on every lane of the row: the
+// lexicographic (value, id) minimum as two reductions -- the value by v_min_f64 stages, then the id
+// among the lanes holding that value by 32-bit v_min_i32 stages -- instead of four stages of a
+// (value, id) pair compare-and-select (measured: 485 cycles of dependent latency per call for the
+// pair form, tools/latency_probe.hip; NaN values are never the minimum, as in the pair form's `<`)
 __device__ __forceinline__ void row_argmin(double& v, int& id) {
-  row_argmin_step(v, id, dppd<kQx1>(v), dppi<kQx1>(id));
-  row_argmin_step(v, id, dppd<kQx2>(v), dppi<kQx2>(id));
-  row_argmin_step(v, id, dppd<kHalfMirror>(v), dppi<kHalfMirror>(id));
-  row_argmin_step(v, id, dppd<kMirror>(v), dppi<kMirror>(id));
+  const double m = row_min(v);
+  id = row_min_i(v == m ? id : 0x7fffffff);
+  v = m;
 }
 
 // min of (v, id) with the partner half / row pair: v_permlane16/32_swap hand each lane its own and
@@ -126,14 +149,30 @@ __device__ __forceinline__ void pair_argmin(double& v, int& id) {
   id = ia;
 }
 
+// min of v / of an int with the partner row (R32: the partner half) by v_permlane16/32_swap
+template <bool R32>
+__device__ __forceinline__ double pair_min(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  auto l = R32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false) : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  auto h = R32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false) : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return fmin(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+}
+template <bool R32>
+__device__ __forceinline__ int pair_min_i(int v) {
+  auto k = R32 ? __builtin_amdgcn_permlane32_swap(v, v, false, false) : __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return min((int)k[0], (int)k[1]);
+}
+
 // reductions over the whole wave: DPP within the 16-lane rows, then the v_permlane16/32_swap
 // exchanges between rows (gfx950) -- no LDS round trip.  A __shfl_xor butterfly costs six
 // ds_bpermute round trips per value; the band kernel's M > 15 classes and the NMPC's M > 15
-// class run several of these per QP iteration
+// class run several of these per QP iteration.  The lexicographic (value, id) minimum as two
+// reductions (value, then the smallest id holding it): 757 cycles of dependent latency per call
+// for the pair form (tools/latency_probe.hip)
 __device__ __forceinline__ void wave_argmin64(double& v, int& id) {
-  row_argmin(v, id);
-  pair_argmin<false>(v, id);
-  pair_argmin<true>(v, id);
+  const double m = pair_min<true>(pair_min<false>(row_min(v)));
+  id = pair_min_i<true>(pair_min_i<false>(row_min_i(v == m ? id : 0x7fffffff)));
+  v = m;
 }
 
 // sum over the four 16-lane rows (lanes l, l+16, l+32, l+48), result in every row:
@@ -171,8 +210,8 @@ __device__ __forceinline__ unsigned long long argkey(double v, int id) {
 }
 template <int CTRL>
 __device__ __forceinline__ unsigned long long dppu64(unsigned long long k) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)k, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(k >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = dpp32<CTRL>((int)(unsigned)k);
+  const int hi = dpp32<CTRL>((int)(unsigned)(k >> 32));
   return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 __device__ __forceinline__ unsigned long long row_minkey(unsigned long long k) {
@@ -209,11 +248,15 @@ __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
 }
 
 #ifdef MPCT_PROFILE
+// diagnostic build: section k's cycles in the low 48 bits of pacc[k], the number of times the
+// section ended in the high 16 (tools/latency_model.py divides one by the other)
+constexpr unsigned long long kProfCount = 1ull << 48;
 #define PSTAMP(k)                                              \
   do {                                                         \
     __builtin_amdgcn_sched_barrier(0);                         \
+    asm volatile("; PSTAMP " #k);                              \
     unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
-    pacc[k] += now_ - pprev;                                   \
+    pacc[k] += now_ - pprev + kProfCount;                      \
     pprev = now_;                                              \
     __builtin_amdgcn_sched_barrier(0);                         \
   } while (0)

@@ -17,8 +17,6 @@ namespace mpct {
 enum OrderKind {
   kOrderGpc = 0,   // GPC / DTC-GPC: QP size M, then the unconstrained move demand (or the weight ratio)
   kOrderNmpc = 1,  // NMPC: horizon N and the weight ratio (fewer Gauss-Newton iterations)
-  kOrderNmpcRows = 2,  // NMPC throughput mode: the M > 15 class first, then N * Nu (nmpc_rows.hip
-                       // groups four consecutive slots per wave)
 };
 
 // per-candidate work bound of the controller-based GPC key (multiply-adds for H); above it the

@@ -40,10 +40,7 @@ __global__ void order_keys(int kind, long long C, int my, int nu, const int* __r
     a /= nu;
     if (kind == kOrderNmpc) {
       k = ~((unsigned)(n2 * nuc) << 14);  // N * Nu: the prediction's length times the QP size
-    } else if (kind == kOrderNmpcRows) {
-      // the one-simulation-per-wave class (M > 15) ahead of the rows' class, so that a wave of the
-      // row kernel holds four row simulations; within each, N * Nu
-      k = ~(((unsigned)(nu * nuc > 15) << 31) | ((unsigned)(n2 * nuc) << 14));
+
     } else {
       const double qd = fmin(fmax((a + 256.0) * 2048.0, 0.0), 1048575.0);
       const unsigned M = (unsigned)(nu * nuc);

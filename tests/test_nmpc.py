@@ -136,7 +136,7 @@ def test_nmpc_scenario_errors(built):
     with pytest.raises(MpctError, match="u_min"):
         nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMAX, nmpc.VDV_UMIN, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 31, 15)
     with pytest.raises(MpctError, match="64 KiB"):
-        nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 400, 16)
+        nmpc.NmpcScenario(x0, nmpc.VDV_U0, nmpc.VDV_UMIN, nmpc.VDV_UMAX, nmpc.VDV_XMIN, nmpc.VDV_XMAX, yref, 400, 15)
 
 
 def test_nmpc_oracle_returned_iterate_drift():
@@ -349,40 +349,3 @@ def test_nmpc_gpu_anderson_reaches_every_optimum(gpu):
         for a, b in ((res.y[s], o.y), (res.u[s], o.u)):
             assert _trel(a, b) < TRAJ_RTOL, (k, _trel(a, b))
         np.testing.assert_allclose(res.J1[s], ((o.y - yref) ** 2).sum(1), rtol=COST_RTOL)
-
-
-@pytest.mark.gpu
-def test_nmpc_gpu_rows_mode_equals_latency_mode(gpu, monkeypatch):
-    """Throughput mode (nmpc_rows.hip: four simulations per wave, one per 16-lane row, for batches of
-    >= 2048) against the latency mode (one simulation per wave with multi-point speculation): the
-    same points, decisions and arithmetic, so the same bits -- the config-5 grid in GAM mode (both
-    QP-size classes: the M > 15 candidates keep one wave each), and a small batch forced into row
-    mode with the open-loop leg and trajectories; and the forced-row batch against the oracle."""
-    import oracle.nmpc_vdv as nv
-    from mpct.engine import eval_batch
-    from mpct.nmpc import nmpc_candidate_grid, vandevusse
-
-    sc, r, yref = vandevusse()
-    N, Nu, d, lam = nmpc_candidate_grid(4096)
-    res = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPCT_NMPC_ROWS", mode)
-        res[mode] = eval_batch(sc, N, Nu, d, lam, r[None])
-    monkeypatch.delenv("MPCT_NMPC_ROWS")
-    a, b = res["1"], res["0"]
-    assert not np.any(a.status & 128)
-    np.testing.assert_array_equal(a.status, b.status)
-    np.testing.assert_array_equal(a.qp_iters, b.qp_iters)
-    np.testing.assert_array_equal(a.J1, b.J1)
-    pick = np.array([0, 1, 2, 3, 5, 8, 13, 21, 34])
-    sm = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPCT_NMPC_ROWS", mode)
-        sm[mode] = eval_batch(sc, N[pick], Nu[pick], d[pick], lam[pick], r[None], open_loop=True, want_traj=True)
-    monkeypatch.delenv("MPCT_NMPC_ROWS")
-    for k in ("J1", "j21", "j22", "Jnu", "status", "qp_iters", "y", "u", "ys", "uopt"):
-        np.testing.assert_array_equal(getattr(sm["1"], k), getattr(sm["0"], k), err_msg=k)
-    for s, k in enumerate(pick[:3]):
-        o = nv.closedloop_nmpc(r, int(N[k]), int(Nu[k]), d[k], lam[k])
-        for x, y in ((sm["1"].y[s], o.y), (sm["1"].u[s], o.u), (sm["1"].uopt[s], o.uopt)):
-            assert _trel(x, y) < TRAJ_RTOL, (k, _trel(x, y))

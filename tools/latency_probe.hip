@@ -3,7 +3,7 @@
 // unrolled chain of each, one wavefront alone on its CU (the latency roofline of
 // the metric kernel, tools/latency_model.py).  Each probe repeats one dependent step kRep times per
 // trip and kTrips trips; cycles per step = (stamp difference) / (kRep * kTrips), minus nothing: the
-// loop overhead is one SALU compare and branch per kRep steps.  Compiled by tools/Makefile.lat:
+// loop overhead is one SALU compare and branch per kRep steps.  Built by hand (not part of build()):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I model-predictive-control-tuning_amd/csrc \
 //         tools/latency_probe.hip -o tools/latency_probe
 // Usage: tools/latency_probe  -> one JSON object {probe: cycles per step}
@@ -15,7 +15,7 @@
 
 using namespace mpct;
 
-constexpr int kRep = 64, kTrips = 64, kProbes = 20;
+constexpr int kRep = 64, kTrips = 64, kProbes = 21;
 
 // keep a value live and opaque to the optimiser (no constant folding across steps)
 __device__ __forceinline__ double opaque(double v) {
@@ -85,6 +85,12 @@ __device__ __forceinline__ double step(double x, double a, double* lds, int lane
       return dppd<kQx1>(x);
     case 18:  // block_prefix<16> at Nu = 5: three DPP row_shr stages with predicated adds
       return block_prefix<16>(x, lane & 7, 5, true, nullptr) * a;
+    case 20: {  // qargmin<16> without the packed key: row_argmin and the lane-0 broadcast (gi_core)
+      int id = lane;
+      double v = x;
+      qargmin<16>(v, id);
+      return v * a + (double)id * 1e-9;
+    }
     default:  // v_mul_f64, dependent
       return x * a;
   }
@@ -121,6 +127,22 @@ static void run(unsigned long long* d) {
   hipLaunchKernelGGL(probe<P>, dim3(1), dim3(64), 0, 0, d, 1.0);
 }
 
+// the shader clock during a busy FP64 loop: s_memtime ticks per s_memrealtime tick (100 MHz)
+__global__ void clock_probe(unsigned long long* out) {
+  double x = opaque(1.0 + threadIdx.x * 1e-9);
+  const double a = opaque(0.9999999);
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < 200000; ++i) x = fma(x, a, 1e-3);
+  x = opaque(x);
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime(), t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    out[0] = t1 - t0;
+    out[1] = r1 - r0;
+    out[2] = (unsigned long long)__double_as_longlong(x);
+  }
+}
+
 int main() {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned long long) * 2 * kProbes) != hipSuccess) return 1;
@@ -128,7 +150,7 @@ int main() {
   for (int rep = 0; rep < 2; ++rep) {  // the first round warms the clocks and the code
     run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d);
     run<9>(d); run<10>(d); run<11>(d); run<12>(d); run<13>(d); run<14>(d); run<15>(d); run<16>(d);
-    run<17>(d); run<18>(d); run<19>(d);
+    run<17>(d); run<18>(d); run<19>(d); run<20>(d);
     if (hipDeviceSynchronize() != hipSuccess) return 2;
   }
   unsigned long long h[2 * kProbes];
@@ -137,11 +159,17 @@ int main() {
                                 "bcast_readlane", "shfl_bpermute", "lds_handoff", "rsq_nr", "rcp_nr",
                                 "row_bcast16", "qargmin16_key", "row_argmin", "wave_argmin64",
                                 "uniform_branch", "ballot_branch", "lds_read_chase", "dpp_mov_pair",
-                                "block_prefix16_nu5", "mul_f64"};
+                                "block_prefix16_nu5", "mul_f64", "qargmin16_exact"};
   printf("{");
   for (int p = 0; p < kProbes; ++p)
     printf("%s\"%s\": %.2f", p ? ", " : "", names[p], (double)h[2 * p] / (kRep * kTrips));
-  printf(", \"steps_per_probe\": %d}\n", kRep * kTrips);
+  unsigned long long* dc = nullptr;
+  if (hipMalloc(&dc, 3 * sizeof(unsigned long long)) != hipSuccess) return 4;
+  hipLaunchKernelGGL(clock_probe, dim3(256), dim3(64), 0, 0, dc);  // every CU busy, like a launch
+  unsigned long long hc[3];
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(hc, dc, sizeof(hc), hipMemcpyDeviceToHost) != hipSuccess)
+    return 5;
+  printf(", \"clock_mhz\": %.1f, \"steps_per_probe\": %d}\n", 100.0 * (double)hc[0] / (double)hc[1], kRep * kTrips);
   (void)hipFree(d);
   return 0;
 }
