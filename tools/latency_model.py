@@ -12,13 +12,25 @@ latency_frac = model / measured.  1.0 would mean the kernel runs at the speed of
 chain with nothing else in the way (issue contention of the SIMD's other waves, instruction issue
 of the off-chain work, LDS bank conflicts, waits the compiler's schedule adds).
 
-Usage: python tools/latency_model.py PROBE.json PROF.bin [--out FILE]
+A second, issue-side figure (--isa): one wave issues at most one VALU instruction per 4 cycles
+(a wave64 instruction occupies the 16-lane SIMD for 4 passes; the dependent FMA latency the probe
+measures is 5.3 cycles), so a section also costs at least 4 x its VALU instructions.  The static
+counts per section come from the profile build's ISA (tools/diag/section_isa.py, minus the stamp's
+own VALU); sections with loops inside (the warm start, the QP entry test in qp(rest)) keep their
+chain price.  issue_frac = sum over sections of max(chain, issue) x executions / measured.
+
+Usage: python tools/latency_model.py PROBE.json PROF.bin [--isa PROF.s] [--out FILE]
   PROF.bin: the per-simulation section words of the profiled heavy batch (MPCT_PROF_OUT)."""
 import argparse
 import json
 import sys
 
+import os
+
 import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "diag"))
+from section_isa import VALU, section_counts  # noqa: E402
 
 SECTIONS = ["prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update", "open_loop",
             "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations"]
@@ -63,6 +75,11 @@ CHAINS = {
 # one Givens rotation of the drop: entries read, a^2 + b^2, rsq + Newton, cs / sn, the RMW of R_A's
 # two rows, lds_sync (gpc_qp16.h:289-310)
 ROTATION = {"lds_handoff": 1, "fma_f64": 1, "rsq_nr": 1, "mul_f64": 1}
+# the profile build's stamp closing each section (section_isa.py names; #1: the QP loop's check)
+ISA_SECTION = {"plant": "PROF_PLANT #0", "y_update": "PROF_YUPD #0", "unconstrained": "PROF_UNC #0",
+               "u_update": "PROF_UUPD #0", "qp.check": "PROF_QCHECK #1", "qp.d+z": "PROF_QD #0",
+               "qp.r+t1": "PROF_QR #0", "qp.add": "PROF_QADD #0", "qp.drop": "PROF_QDROP #0"}
+STAMP_VALU = 6  # ProfAcc.add: lane id copy, compare, two selects, 64-bit add (wave_ops.h)
 
 
 def chain_cycles(chain, lat):
@@ -73,8 +90,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("probe")
     ap.add_argument("prof")
+    ap.add_argument("--isa", default=None)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    valu = {}
+    if a.isa:
+        for closer, row in section_counts(a.isa, "gpc_small_kernel"):
+            valu.setdefault(closer, sum(row.get(c, 0) for c in VALU) - STAMP_VALU)
     lat = json.load(open(a.probe))
     raw = np.fromfile(a.prof, dtype=np.uint64)
     width = len(SECTIONS) if raw.size % len(SECTIONS) == 0 and raw.size % 13 else 13  # pre-r05 dumps: 13
@@ -83,22 +105,32 @@ def main():
     cnt = (raw >> np.uint64(48)).astype(np.float64)
     S = raw.shape[0]
     rows = {}
-    model = measured = 0.0
+    model = measured = bound = 0.0
     for k, name in enumerate(SECTIONS):
         if name not in CHAINS:
             continue
         per = chain_cycles(CHAINS[name], lat)
         n = cnt[:, k].mean()
+        if name == "qp.check":  # the QP's entry stamp closes a near-empty section once per step
+            n -= cnt[:, SECTIONS.index("plant")].mean()
         m = cyc[:, k].mean()
         mod = per * n
         if name == "qp.drop" and width > 13:  # plus the counted Givens rotations of every drop
             mod += chain_cycles(ROTATION, lat) * cnt[:, SECTIONS.index("qp.rotations")].mean()
         rows[name] = dict(executions=round(n, 1), chain_cycles=round(per, 1), model=round(mod),
                           measured=round(m), frac=round(mod / m, 3) if m else None)
+        b = mod
+        if name in ISA_SECTION and ISA_SECTION[name] in valu:
+            iss = 4.0 * valu[ISA_SECTION[name]]
+            b = max(per, iss) * n + (mod - per * n)
+            rows[name].update(valu_static=valu[ISA_SECTION[name]], issue_cycles=round(iss),
+                              bound=round(b), bound_frac=round(b / m, 3) if m else None)
         model += mod
+        bound += b
         measured += m
     rep = dict(simulations=int(S), probe=a.probe, model_cycles=round(model), measured_cycles=round(measured),
-               latency_frac=round(model / measured, 3), sections=rows,
+               latency_frac=round(model / measured, 3),
+               issue_frac=round(bound / measured, 3) if valu else None, sections=rows,
                note="measured excludes the prologue (once per simulation); cycles per simulation, mean over "
                     "the batch; stamps add ~11 % to the measured side (MI355X_MICROARCH.md)")
     print(json.dumps(rep, indent=1))
