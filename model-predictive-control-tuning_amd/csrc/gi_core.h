@@ -138,16 +138,25 @@ __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int 
 struct RAFull {
   int M;
   static constexpr bool packed = false;
+  static constexpr bool store = true;
   __device__ __forceinline__ int operator()(int i, int j) const { return i * M + j; }
 };
 struct RAPacked {
   static constexpr bool packed = true;
+  static constexpr bool store = true;
   // 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate): j <= 64
   __device__ __forceinline__ int operator()(int i, int j) const {
     return (int)(__umul24((unsigned)j, (unsigned)(j + 3)) >> 1) + i;
   }
 };
 __host__ __device__ constexpr int ra_packed_size(int M) { return (M * (M + 3)) / 2; }
+// no R_A at all: the caller keeps B = R_A^-1 instead (the band kernel's widest class, which drops
+// constraints with rotations derived from B); gi_add then writes no R_A entry
+struct RANone {
+  static constexpr bool packed = true;
+  static constexpr bool store = false;
+  __device__ __forceinline__ int operator()(int, int) const { return 0; }
+};
 
 // r = R_A^-1 c  (c_w in lane w < q): column back substitution, lane w ends with r_w
 template <int MAXM, class RAL>
@@ -173,11 +182,21 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
   return gi_backsub<MAXM>(S, sRA, M, c, RAFull{M});
 }
 
+// extra factors a caller keeps in step with R_A (the band kernel's explicit R_A^-1): gi_add calls
+// add(q, 1 / alpha) for the new column q, gi_drop calls rot(jj, q, cs, sn) with every Givens
+// rotation of R_A's rows (jj, jj + 1) and drop_rows(kd, q) after the last one, each before the
+// lds_sync that ends the step
+struct GINoExt {
+  __device__ __forceinline__ void add(int, double) const {}
+  __device__ __forceinline__ void rot(int, int, double, double) const {}
+  __device__ __forceinline__ void drop_rows(int, int) const {}
+};
+
 // append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
-template <int MAXM, class Mark, class RAL>
+template <int MAXM, class Mark, class RAL, class Ext = GINoExt>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
-                                       const Mark& mark, const RAL& ra) {
+                                       const Mark& mark, const RAL& ra, const Ext& ext = Ext{}) {
   const int lane = qp_lane();
   const int q = S.q;
   const double dq = bcast(dk, q);
@@ -201,14 +220,17 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
     }
     for (; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
-  if (lane < q) sRA[ra(lane, q)] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  if constexpr (RAL::store) {
+    if (lane < q) sRA[ra(lane, q)] = dk;  // new column q of R_A = [d(0:q-1); alpha]
+  }
   const double ia = qp_rcp(alpha);
   if (lane == q) {
-    sRA[ra(q, q)] = alpha;
+    if constexpr (RAL::store) sRA[ra(q, q)] = alpha;
     S.rdg = ia;
     S.uw = upm;
     S.ww = p;
   }
+  ext.add(q, ia);
   mark(S, p, true);
   S.q = q + 1;
   S.nrot += 1;
@@ -222,9 +244,9 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
 }
 
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
-template <int MAXM, class Mark, class RAL>
+template <int MAXM, class Mark, class RAL, class Ext = GINoExt>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
-                                        const Mark& mark, const RAL& ra) {
+                                        const Mark& mark, const RAL& ra, const Ext& ext = Ext{}) {
   const int lane = qp_lane();
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
@@ -261,11 +283,13 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
           sJT[jj * M + lane] = cs * j0v + sn * j1v;
           sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
         }
+        ext.rot(jj, q, cs, sn);
         S.nrot += 1;
       }
       lds_sync();
     }
   }
+  ext.drop_rows(kd, q);
   const int qn = q - 1;
   if (lane == qn) {
     S.uw = 0.0;

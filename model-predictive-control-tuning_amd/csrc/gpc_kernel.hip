@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
   const int M = nu * Nu;
   int st = 0;
 #ifdef MPCT_PROFILE
-  unsigned long long pacc[PROF_N] = {};
+  ProfAcc pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef MPCT_TIMELINE
@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
   }
 #ifdef MPCT_PROFILE
   if (lane == 0 && out.prof)
-    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc.get(k);
 #endif
 #ifdef MPCT_TIMELINE
   if (lane == 0 && out.prof) {

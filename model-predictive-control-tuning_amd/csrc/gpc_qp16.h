@@ -189,12 +189,25 @@ __device__ __forceinline__ void gi16_load_rinv(GIState<16>& S, RegFactors& F, co
   S.jinit = true;
 }
 
-// d = J'n_p for constraint p (rows j0..mp of J, sign sg) -> column vector
+// d = J'n_p for constraint p (rows j0..mp of J, sign sg) -> column vector.  A one-row normal (the
+// rate rows, kinds 0/1) is row j0 of J itself: fetched by ds_bpermute (8 instructions) instead of
+// the 16-lane sum of the masked rows (48), the same value
+#ifndef MPCT_QP16_SUM4
+#define MPCT_QP16_SUM4 1
+#endif
+#ifndef MPCT_QP16_DVEC_BPERM
+#define MPCT_QP16_DVEC_BPERM 1
+#endif
 __device__ __forceinline__ void gi16_dvec(const RegFactors& F, int j0, int mp, double sg, d4v& d) {
   const int i = q16_i();
-  const bool in = i >= j0 && i <= mp;
-  FOR4(r, d[r] = in ? F.J[r] : 0.0;);
-  row16_sum4(d);
+  if (MPCT_QP16_DVEC_BPERM && j0 == mp) {
+    const int src = j0 + 16 * q16_b();
+    FOR4(r, d[r] = __shfl(F.J[r], src, kWave););
+  } else {
+    const bool in = i >= j0 && i <= mp;
+    FOR4(r, d[r] = in ? F.J[r] : 0.0;);
+    row16_sum4(d);
+  }
   FOR4(r, d[r] *= sg;);
 }
 
@@ -217,10 +230,18 @@ __device__ __forceinline__ void gi16_products(const RegFactors& F, const d4v& Bl
     }
   });
   const double jl = (b == (q >> 2)) ? sel4u(F.J, q & 3) : 0.0;
+#if MPCT_QP16_SUM4
+  z = za;
+  jq = jl;
+  rk = ra;
+  dn2 = s1;
+  row4_sum4(z, jq, rk, dn2);  // bitwise the four row4_sums, 21 instructions instead of 40
+#else
   z = row4_sum(za);
   jq = row4_sum(jl);
   rk = row4_sum(ra);
   dn2 = row4_sum(s1);
+#endif
   beta = row4_sum(s2);
 }
 
@@ -330,7 +351,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
                                        int* st, GIState<16>& S, RegFactors& F, int rebuild, double& xout
 #ifdef MPCT_PROFILE
-                                       , unsigned long long* pacc, unsigned long long& pprev
+                                       , ProfAcc& pacc, unsigned long long& pprev
 #endif
                                        ) {
   const int lane = qlane(), i = lane & 15;
@@ -423,8 +444,14 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
             la = fma(Bl[r], w[r], la);
           }
         });
+#if MPCT_QP16_SUM4
+        row4_sum2(xa, la);
+        xm = xu + xa;
+        const double lam = la;
+#else
         xm = xu + row4_sum(xa);
         const double lam = row4_sum(la);
+#endif
         if (i < q) S.uw = lam;
         double lmin = i < q ? lam : INFINITY;
         int kd = i;

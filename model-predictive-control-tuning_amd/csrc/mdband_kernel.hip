@@ -58,6 +58,14 @@ constexpr double kRelTol = MPCT_BAND_RELTOL;
 #define MPCT_BAND_RN_F64 0
 #endif
 typedef std::conditional_t<MPCT_BAND_RN_F64 != 0, double, float> rn_t;
+// the widest class (Mz > 32, MAXM = 64) keeps B = R_A^-1 instead of R_A, in R_A's packed place
+// (band_drop_b): the dual direction r = R_A^-1 d, the warm start's R_A'w = c and lambda = R_A^-1 w
+// become products over the active set instead of serial substitutions (one broadcast per active
+// constraint, q ~ 41 on config 3's slowest simulations), and a drop's rotations come from B's row
+// instead of a chain of LDS round trips through R_A.  MPCT_BAND_EXB=0 keeps R_A in every class
+#ifndef MPCT_BAND_EXB
+#define MPCT_BAND_EXB 1
+#endif
 
 namespace mpct {
 
@@ -83,6 +91,7 @@ __host__ __device__ inline int pow2_at_least(int n) {
 // instead of an LDS copy: 21.5 KB less LDS at N2 = 127, 3.14 -> 3.09 s
 constexpr long long kBandCapsKb[] = {20, 26, 32, 40, 53, 80, 160};
 
+
 // full_ri: R^-1 is a full triangle (some OV weight > 0); in band mode R is diagonal and only its
 // inverse diagonal is kept.  ncopy: 2 with the open-loop prediction (a second plant copy), else 1
 __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2, int M, bool full_ri = true,
@@ -93,7 +102,7 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.ri = take(full_ri ? Mz * Mz : Mz);
   L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
-  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked)
+  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked); B = R_A^-1 there when MAXM = 64
   L.dv = take(Mz);       // d = J'n
   L.nv = take(Mz);       // staged normal n_p
   L.xc = take(Mz);       // QP iterate
@@ -124,6 +133,146 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.mza = take(ne * sc.mz_maxa);
   L.total = (o + 1) & ~1;
   return L;
+}
+
+// B = R_A^-1 of the band kernel's widest class, in R_A's packed layout (gi_core.h RAPacked: column
+// k holds rows 0..k+1).  Entry (k + 1, k) is kept zero on the active block, and bt_mul / bt_tmul
+// read it in place of every entry below the stored ones.
+__device__ __forceinline__ int bt_idx(int w, int k) { return (int)(__umul24((unsigned)k, (unsigned)(k + 3)) >> 1) + w; }
+// gi_add's hook: column q = [-r / alpha; 1 / alpha] (r = R_A^-1 d(0:q), the iteration's dual
+// direction), the stored entries below the diagonal next to it zeroed
+struct BandBAdd {
+  double* bt;
+  double r;  // this lane's r_w
+  __device__ __forceinline__ void add(int q, double ia) const {
+    const int lane = threadIdx.x;
+    if (lane < q) bt[bt_idx(lane, q)] = -r * ia;
+    else if (lane == q) bt[bt_idx(q, q)] = ia;
+    if (lane == q && q > 0) bt[bt_idx(q, q - 1)] = 0.0;
+    if (lane == q + 1) bt[bt_idx(q + 1, q)] = 0.0;
+  }
+  __device__ __forceinline__ void rot(int, int, double, double) const {}
+  __device__ __forceinline__ void drop_rows(int, int) const {}
+};
+// lane w < q: sum_{k < q} B(w,k) c_k, c in LDS
+__device__ __forceinline__ double bt_mul(const double* bt, const double* c, int q) {
+  const int lane = threadIdx.x;
+  double r0 = 0.0, r1 = 0.0;
+  if (lane < q) {
+    auto b = [&](int k) __attribute__((always_inline)) { return bt[bt_idx(min(lane, k + 1), k)]; };
+    int k = 0;
+    for (; k + 3 < q; k += 4) {
+      const double b0 = b(k), b1 = b(k + 1), b2 = b(k + 2), b3 = b(k + 3);
+      const double c0 = c[k], c1 = c[k + 1], c2 = c[k + 2], c3 = c[k + 3];
+      r0 = fma(b0, c0, r0);
+      r1 = fma(b1, c1, r1);
+      r0 = fma(b2, c2, r0);
+      r1 = fma(b3, c3, r1);
+    }
+    for (; k < q; ++k) r0 = fma(b(k), c[k], r0);
+  }
+  return r0 + r1;
+}
+// lane v < q: (B'c)_v = sum_{k < q} B(k,v) c_k, i.e. w with R_A'w = c
+__device__ __forceinline__ double bt_tmul(const double* bt, const double* c, int q) {
+  const int lane = threadIdx.x;
+  double r0 = 0.0, r1 = 0.0;
+  if (lane < q) {
+    const double* col = bt + bt_idx(0, lane);
+    auto b = [&](int k) __attribute__((always_inline)) { return col[min(k, lane + 1)]; };
+    int k = 0;
+    for (; k + 3 < q; k += 4) {
+      const double b0 = b(k), b1 = b(k + 1), b2 = b(k + 2), b3 = b(k + 3);
+      const double c0 = c[k], c1 = c[k + 1], c2 = c[k + 2], c3 = c[k + 3];
+      r0 = fma(b0, c0, r0);
+      r1 = fma(b1, c1, r1);
+      r0 = fma(b2, c2, r0);
+      r1 = fma(b3, c3, r1);
+    }
+    for (; k < q; ++k) r0 = fma(b(k), c[k], r0);
+  }
+  return r0 + r1;
+}
+// inclusive prefix sum over the wave's lanes: DPP row_shr within each 16-lane row, then the row
+// totals (readlane) carried into the rows above
+__device__ __forceinline__ double wave_prefix_sum(double v) {
+  const int i = threadIdx.x & 15, b = threadIdx.x >> 4;
+  double t;
+  t = dppd<0x111>(v); if (i >= 1) v += t;
+  t = dppd<0x112>(v); if (i >= 2) v += t;
+  t = dppd<0x114>(v); if (i >= 4) v += t;
+  t = dppd<0x118>(v); if (i >= 8) v += t;
+  const double t0 = bcast(v, 15), t1 = bcast(v, 31), t2 = bcast(v, 47);
+  if (b >= 1) v += t0;
+  if (b >= 2) v += t1;
+  if (b >= 3) v += t2;
+  return v;
+}
+// remove active constraint kd with B alone.  R_A E (column kd removed) is re-triangularised by
+// rotations G on rows (jj, jj + 1), jj = kd..q-2; then B_new = (B G')[rows != kd, columns < q-1],
+// which is upper triangular exactly when G turns B's row kd into a multiple of e_{q-1} (row kd of
+// B G' times R_new = row kd of E = 0).  So rotation jj zeroes the running entry x of row kd against
+// y = B(kd, jj + 1): cs = y / r, sn = -x / r, r = |row kd (kd..jj+1)|, all from one prefix sum of
+// B(kd, .)^2 -- no serial chain of LDS round trips (the R_A form's rsq + RMW + lds_sync per
+// rotation).  The same rotations go to J's columns; each lane then sweeps its row of J and of B
+// through them with the running entry in a register, writing B's rows kd + 1.. one row up.
+// The same factorisation as the R_A form up to the signs of R_new's rows (Givens QR is unique up
+// to them), which J and B carry consistently.  cs / sn are staged in sc_ / ss_ (Mz doubles each).
+template <class Mark>
+__device__ __forceinline__ void band_drop_b(GIState<64>& S, double* sJT, double* bt, int Mz, int kd,
+                                            const Mark& mark, double* sc_, double* ss_) {
+  const int lane = threadIdx.x;
+  const int q = S.q;
+  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
+  mark(S, idk, false);
+  {
+    const double un = lane_next<64>(S.uw);
+    const int wn = lane_next_i<64>(S.ww);
+    if (lane >= kd && lane < q - 1) {
+      S.uw = un;
+      S.ww = wn;
+    }
+  }
+  // rotation parameters: lane jj in [kd, q-2]
+  const double y = (lane >= kd && lane < q) ? bt[bt_idx(kd, lane)] : 0.0;
+  const double s2 = wave_prefix_sum(y * y);  // lane j: |B(kd, kd..j)|^2
+  const double yn = lane_next<64>(y), r2 = lane_next<64>(s2);
+  if (lane >= kd && lane < q - 1) {
+    const double x = lane == kd ? y : (s2 > 0.0 ? s2 * rsq_nr(s2) : 0.0);
+    double cs = 1.0, sn = 0.0;
+    if (r2 > 0.0) {
+      const double ri = rsq_nr(r2);
+      cs = yn * ri;
+      sn = -x * ri;
+    }
+    sc_[lane] = cs;
+    ss_[lane] = sn;
+  }
+  lds_sync();
+  // J's columns (lanes = rows of J) and B's rows by slot (lanes = rows w < q)
+  const bool jrow = lane < Mz, brow = lane < q;
+  double cj = jrow ? sJT[kd * Mz + lane] : 0.0;
+  double cb = (brow && lane <= kd + 1) ? bt[bt_idx(lane, kd)] : 0.0;
+  const int wdst = lane > kd ? lane - 1 : lane;  // B's row kd leaves: rows below move up one
+  for (int jj = kd; jj < q - 1; ++jj) {
+    const double cs = sc_[jj], sn = ss_[jj];
+    const double nj = jrow ? sJT[(jj + 1) * Mz + lane] : 0.0;
+    const double nb = (brow && lane <= jj + 2) ? bt[bt_idx(min(lane, jj + 2), jj + 1)] : 0.0;
+    if (jrow) sJT[jj * Mz + lane] = cs * cj + sn * nj;
+    const double vb = cs * cb + sn * nb;
+    if (brow && lane != kd && wdst <= jj + 1) bt[bt_idx(wdst, jj)] = vb;
+    cj = -sn * cj + cs * nj;
+    cb = -sn * cb + cs * nb;
+  }
+  if (jrow) sJT[(q - 1) * Mz + lane] = cj;
+  const int qn = q - 1;
+  if (lane == qn) {
+    S.uw = 0.0;
+    S.ww = -1;
+  }
+  S.nrot += q - 1 - kd;
+  S.q = qn;
+  lds_sync();
 }
 
 // active flags: box rows (p < 4*Mz) in the lanes' act bits, output rows in the LDS bitmap
@@ -161,7 +310,7 @@ __global__ void __launch_bounds__(64, 1)
   const int P = my * N2;
   int st = 0;
 #ifdef MPCT_PROFILE
-  unsigned long long pacc[PROF_N] = {};
+  ProfAcc pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -202,6 +351,8 @@ __global__ void __launch_bounds__(64, 1)
   double* sJT = lds + L.jt;
   double* sRA = lds + L.ra;
   const RAPacked rap{};
+  constexpr bool EXB = MPCT_BAND_EXB != 0 && MAXM == 64;  // B = R_A^-1 in R_A's place (band_drop_b)
+  double* sBT = lds + L.ra;
   double* sd = lds + L.dv;
   double* snv = lds + L.nv;
   double* sxc = lds + L.xc;
@@ -616,7 +767,11 @@ __global__ void __launch_bounds__(64, 1)
           lds_sync();
           const double zm = gi_z(sJT, sd, v, Mz, row);
           const double uk = gis.uw;
-          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap);
+          if constexpr (EXB)
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, RANone{},
+                         BandBAdd{sBT, bt_mul(sBT, sd, v)});
+          else
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap);
           if (lane == v) gis.uw = uk;
           ++it;
         }
@@ -640,26 +795,49 @@ __global__ void __launch_bounds__(64, 1)
         }
         double wv = 0.0;
         x = row ? xu : 0.0;
-        // R_A'w = c, x = x_u + J(:,0:q) w; step v's R_A and J entries are loaded one step ahead,
-        // off the chain of broadcasts
-        double ra = lane < Mz ? sRA[rap(0, lane)] : 0.0, jv = row ? sJT[lane] : 0.0;
-        for (int v = 0; v < q; ++v) {
-          const int vn = v + 1 < q ? v + 1 : v;
-          const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
-          const double w = bcast(cc * gis.rdg, v);
-          if (lane == v) wv = w;
-          if (lane > v && lane < q) cc -= ra * w;
-          if (row) x += jv * w;
-          ra = ran;
-          jv = jvn;
+        double lam;
+        if constexpr (EXB) {
+          // w = B'c, then x = x_u + J(:,0:q) w and lambda = B w, three products (w staged in sd)
+          if (row) snv[lane] = cc;
+          lds_sync();
+          wv = bt_tmul(sBT, snv, q);
+          if (row) sd[lane] = lane < q ? wv : 0.0;
+          lds_sync();
+          if (row) {
+            double x1 = 0.0;
+            int v = 0;
+            for (; v + 1 < q; v += 2) {
+              x = fma(sJT[v * Mz + lane], sd[v], x);
+              x1 = fma(sJT[(v + 1) * Mz + lane], sd[v + 1], x1);
+            }
+            if (v < q) x = fma(sJT[v * Mz + lane], sd[v], x);
+            x += x1;
+          }
+          lam = bt_mul(sBT, sd, q);
+          lds_sync();  // sd / snv are rewritten by the next dvec or pass
+        } else {
+          // R_A'w = c, x = x_u + J(:,0:q) w; step v's R_A and J entries are loaded one step ahead,
+          // off the chain of broadcasts
+          double ra = lane < Mz ? sRA[rap(0, lane)] : 0.0, jv = row ? sJT[lane] : 0.0;
+          for (int v = 0; v < q; ++v) {
+            const int vn = v + 1 < q ? v + 1 : v;
+            const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
+            const double w = bcast(cc * gis.rdg, v);
+            if (lane == v) wv = w;
+            if (lane > v && lane < q) cc -= ra * w;
+            if (row) x += jv * w;
+            ra = ran;
+            jv = jvn;
+          }
+          lam = gi_backsub<MAXM>(gis, sRA, Mz, wv, rap);
         }
-        const double lam = gi_backsub<MAXM>(gis, sRA, Mz, wv, rap);
         if (lane < q) gis.uw = lam;
         double lmin = lane < q ? lam : INFINITY;
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap);
+        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, kd, mark, snv, sd);
+        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap);
         ++it;
       }
       return row ? x : 0.0;
@@ -732,7 +910,9 @@ __global__ void __launch_bounds__(64, 1)
         lds_sync();
         const double zm = gi_z(sJT, sd, gis.q, Mz, row);
         PSTAMP(PROF_QD);
-        const double rk = gi_backsub<MAXM>(gis, sRA, Mz, dk, rap);
+        double rk;
+        if constexpr (EXB) rk = bt_mul(sBT, sd, gis.q);
+        else rk = gi_backsub<MAXM>(gis, sRA, Mz, dk, rap);
         double t1 = INFINITY;
         int kdrop = 0x7fffffff;
         if (lane < gis.q && rk > 0.0) {
@@ -754,11 +934,15 @@ __global__ void __launch_bounds__(64, 1)
         upm += t;
         sp += t * beta;
         if (full) {
-          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap);
+          if constexpr (EXB)
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk});
+          else
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap);
           PSTAMP(PROF_QADD);
           break;
         }
-        gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap);
+        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, kdrop, mark, snv, sd);
+        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap);
         PSTAMP(PROF_QDROP);
         if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;
@@ -985,7 +1169,7 @@ __global__ void __launch_bounds__(64, 1)
 #ifdef MPCT_PROFILE
   PSTAMP(PROF_PLANT);
   if (lane == 0 && out.prof)
-    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc.get(k);
 #endif
   // ------------------------------------------------------------------ results
   if (lane < my) {
@@ -1034,7 +1218,11 @@ static int launch_band_t(const DevScenario& sc, long long C, int nref, const int
                          std::string* err) {
   const int nu_hi = std::min(sc.numax, (MAXM - 1) / sc.nu);
   if (nu_hi < 1) return 0;
-  const long long lds_max = mdband_lds_bytes(sc, sc.n2max, nu_hi, o.open_loop ? 2 : 1);
+  // the largest simulation of the class (over every N2 and Nu: no monotonicity assumed)
+  long long lds_max = 0;
+  for (int nu_c = 1; nu_c <= nu_hi; ++nu_c)
+    for (int n2 = 1; n2 <= sc.n2max; ++n2)
+      lds_max = std::max(lds_max, mdband_lds_bytes(sc, n2, nu_c, o.open_loop ? 2 : 1));
   if (lds_max > 160 * 1024) {
     *err = "scenario needs more than 160 KiB of LDS per simulation";
     return -4;

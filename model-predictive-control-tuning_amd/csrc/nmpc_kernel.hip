@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64, 1)
   int st = 0;
 #ifdef MPCT_PROFILE
   // diagnostic build: section cycle sums (tools/nmpc_latency.py --profile; labels: mpct_host.cpp)
-  unsigned long long pacc[PROF_N] = {};
+  ProfAcc pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -754,7 +754,7 @@ __global__ void __launch_bounds__(64, 1)
 #ifdef MPCT_PROFILE
   PSTAMP(PROF_NM_OTHER);
   if (lane == 0 && out.prof)
-    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc[k];
+    for (int k = 0; k < PROF_N; ++k) out.prof[sim * PROF_N + k] = pacc.get(k);
 #endif
   // ------------------------------------------------------------------ results
   if (lane < ny) {

@@ -54,12 +54,20 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // row_half_mirror, row_newbcast) use v_mov_b32_dpp without an `old` operand: the update_dpp(0, ..)
 // form makes the compiler zero a fresh register before every move (two v_mov_b32 per double,
 // ~60 per Goldfarb-Idnani step of the metric kernel).  The row shifts (row_shl / row_shr: lanes at
-// the row's edge have no source) keep old = 0; their callers never read those lanes.
+// the row's edge have no source) set bound_ctrl, which writes 0 to those lanes as old = 0 would,
+// without the zeroed register; MPCT_DPP_OLD0=1 restores update_dpp(0, ..) for them
+#ifndef MPCT_BP_BRANCHY
+#define MPCT_BP_BRANCHY 0
+#endif
+#ifndef MPCT_DPP_OLD0
+#define MPCT_DPP_OLD0 0
+#endif
 template <int CTRL>
 constexpr bool kDppAllLanes = CTRL < 0x100 || CTRL == 0x140 || CTRL == 0x141 || (CTRL >= 0x150 && CTRL <= 0x15F);
 template <int CTRL>
 __device__ __forceinline__ int dpp32(int v) {
   if constexpr (kDppAllLanes<CTRL>) return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+  else if constexpr (MPCT_DPP_OLD0 == 0) return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
   else return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
 template <int CTRL>
@@ -189,6 +197,50 @@ __device__ __forceinline__ double row4_sum(double v) {
   return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
 }
 
+// row4_sum of two / four values at once, bitwise equal to row4_sum of each ((v0 + v1) + (v2 + v3)):
+// the first swaps pair different values, so they need no register copies (v_permlane*_swap
+// overwrites both operands), and the partial sums travel together until one final broadcast.
+// Two values: 12 instructions instead of 20; four: 21 instead of 40
+__device__ __forceinline__ void permlane16_pair(double& x, double& y) {  // x, y <- rows (0 2 | 1 3) mix
+  auto l = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
+  auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
+  x = __hiloint2double(h[0], l[0]);
+  y = __hiloint2double(h[1], l[1]);
+}
+__device__ __forceinline__ void permlane32_pair(double& x, double& y) {
+  auto l = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
+  auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
+  x = __hiloint2double(h[0], l[0]);
+  y = __hiloint2double(h[1], l[1]);
+}
+__device__ __forceinline__ void row4_sum2(double& a, double& b) {
+  permlane16_pair(a, b);  // a = [a0 b0 a2 b2], b = [a1 b1 a3 b3]
+  double p = a + b;       // [a01 b01 a23 b23]
+  double q = p;
+  permlane32_pair(p, q);  // p = [a01 b01 a01 b01], q = [a23 b23 a23 b23]
+  p += q;                 // [A B A B]
+  q = p;
+  permlane16_pair(p, q);  // p = [A A A A], q = [B B B B]
+  a = p;
+  b = q;
+}
+__device__ __forceinline__ void row4_sum4(double& a, double& b, double& c, double& d) {
+  permlane16_pair(a, b);
+  permlane16_pair(c, d);
+  double p = a + b, q = c + d;  // p = [a01 b01 a23 b23], q = [c01 d01 c23 d23]
+  permlane32_pair(p, q);        // p = [a01 b01 c01 d01], q = [a23 b23 c23 d23]
+  double v = p + q;             // [A B C D]
+  double w = v;
+  permlane16_pair(v, w);        // v = [A A C C], w = [B B D D]
+  double v2 = v, w2 = w;
+  permlane32_pair(v, v2);       // v = [A A A A], v2 = [C C C C]
+  permlane32_pair(w, w2);       // w = [B B B B], w2 = [D D D D]
+  a = v;
+  b = w;
+  c = v2;
+  d = w2;
+}
+
 __device__ __forceinline__ double wave_sum64(double v) { return row4_sum(row_sum(v)); }
 
 // reductions over the QP-row lanes (0..M-1): DPP within row 0 when the template allows M <= 16
@@ -222,10 +274,18 @@ __device__ __forceinline__ unsigned long long row_minkey(unsigned long long k) {
   return k;
 }
 
+// MPCT_PACKED_ARGMIN=1 restores the packed-key form for the callers that pass `shift` (round 2:
+// five VALU instructions per stage against about ten for the (value, id) pair compare of the time).
+// Measured per call as a dependent chain (tools/latency_probe.hip, r05): packed key 281 cycles,
+// row_argmin (value min, then id min) plus the lane-0 broadcast 197 cycles, so the exact form is
+// the default; it also selects exactly the lexicographic (value, id) minimum
+#ifndef MPCT_PACKED_ARGMIN
+#define MPCT_PACKED_ARGMIN 0
+#endif
 template <int MAXM>
 __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
   if constexpr (MAXM <= 16) {
-    if (shift >= 0) {
+    if (MPCT_PACKED_ARGMIN && shift >= 0) {
       // lanes >= 16 hold INF (callers), so row 0's minimum is the QP rows' minimum
       const unsigned long long k = row_minkey(argkey(v, id));
       const int kid = (int)(__builtin_amdgcn_readlane((int)(unsigned)k, 0) & 63);
@@ -251,6 +311,28 @@ __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
 // diagnostic build: section k's cycles in the low 48 bits of pacc[k], the number of times the
 // section ended in the high 16 (tools/latency_model.py divides one by the other)
 constexpr unsigned long long kProfCount = 1ull << 48;
+// the section words live in one 64-bit VGPR pair, lane k holding word k: an SGPR array of PROF_N
+// words (the first form) was copied whole at every loop back-edge of the step loop (28 s_mov per
+// QP iteration), which inflated the sections it was measuring
+struct ProfAcc {
+  unsigned long long v = 0;
+  struct Ref {
+    ProfAcc* a;
+    int k;
+    __device__ __forceinline__ void operator+=(unsigned long long d) { a->add(k, d); }
+  };
+  __device__ __forceinline__ Ref operator[](int k) { return Ref{this, k}; }
+  __device__ __forceinline__ void add(int k, unsigned long long d) {
+    int l = threadIdx.x;
+    asm volatile("" : "+v"(l));
+    v += (l == k) ? d : 0ull;
+  }
+  __device__ __forceinline__ unsigned long long get(int k) const {  // wave-uniform
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, k);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), k);
+    return ((unsigned long long)hi << 32) | lo;
+  }
+};
 #define PSTAMP(k)                                              \
   do {                                                         \
     __builtin_amdgcn_sched_barrier(0);                         \
@@ -289,10 +371,18 @@ __device__ __forceinline__ int lane_next_i(int v) {
 template <int MAXM>
 __device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row, double* sxc) {
   if constexpr (MAXM <= 16) {
+    // the first three stages run whatever Nu is (l < Nu masks them): their uniform Nu tests were
+    // four SALU / VALU instructions and a branch each, more than the stage they skip
     double pre = x, t;
+#if MPCT_BP_BRANCHY
     if (Nu > 1) { t = dppd<0x111>(pre); if (l >= 1) pre += t; }
     if (Nu > 2) { t = dppd<0x112>(pre); if (l >= 2) pre += t; }
     if (Nu > 4) { t = dppd<0x114>(pre); if (l >= 4) pre += t; }
+#else
+    t = dppd<0x111>(pre); if (l >= 1) pre += t;
+    t = dppd<0x112>(pre); if (l >= 2) pre += t;
+    t = dppd<0x114>(pre); if (l >= 4) pre += t;
+#endif
     if (Nu > 8) { t = dppd<0x118>(pre); if (l >= 8) pre += t; }
     return pre;
   } else {
