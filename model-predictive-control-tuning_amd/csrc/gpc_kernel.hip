@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
   const int M = nu * Nu;
   int st = 0;
 #ifdef MPCT_PROFILE
-  ProfAcc pacc;
+  ProfAccS pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef MPCT_TIMELINE

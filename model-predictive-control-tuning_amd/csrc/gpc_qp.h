@@ -37,7 +37,7 @@ template <int MAXM>
 __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCons& rc, double up_row,
                      double xu, double tol, int maxit, int* st, GIState<MAXM>& S
 #ifdef MPCT_PROFILE
-                     , ProfAcc& pacc, unsigned long long& pprev
+                     , ProfAccS& pacc, unsigned long long& pprev
 #endif
                      ) {
   const int lane = qp_lane();

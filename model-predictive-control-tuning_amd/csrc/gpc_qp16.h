@@ -50,6 +50,12 @@ struct RegFactors {
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
 // candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
 constexpr int kBS = 16;
+// 1: drops from B alone (gi16_drop_b), no R_A kept; 0: R_A in LDS and its Givens chain (gi16_drop).
+// Measured the same at 4096 candidates and 1 % slower on the heaviest 256 (gpurun_out/r05l): the
+// metric's drops average three rotations, and J's register rotations dominate them either way
+#ifndef MPCT_QP16_BDROP
+#define MPCT_QP16_BDROP 0
+#endif
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
@@ -268,7 +274,7 @@ __device__ __forceinline__ void gi16_add(GIState<16>& S, RegFactors& F, double* 
   if (lane <= q) F.sB[lane * kBS + q] = lane < q ? -rk * ia : ia;
   if (lane < q) F.sB[q * kBS + lane] = 0.0;
   // R_A(w, q) = d_w (w < q), R_A(q, q) = alpha: lanes (i < 4, b) write entry 4b + i
-  {
+  if (!MPCT_QP16_BDROP) {
     const int w = 4 * b + i;
     if (i < 4 && w < q) sRA[w * M + q] = sel4v(d, i);
     if (lane == 0) sRA[q * M + q] = alpha;
@@ -342,16 +348,71 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
   lds_sync();
 }
 
+// remove active constraint kd with B = R_A^-1 alone (the band kernel's band_drop_b, DESIGN §11
+// round 5): R_A E (column kd removed) is re-triangularised by rotations on rows (jj, jj + 1) that
+// turn B's row kd into a multiple of e_{q-1}; rotation jj zeroes the running entry x of that row
+// against y = B(kd, jj + 1), cs = y / r, sn = -x / r, r = |B(kd, kd..jj+1)|, all from one 16-lane
+// prefix sum.  J's columns take the rotations in registers as before; each lane w < q sweeps its
+// row of B through them with the running entry in a register and writes it one row up below kd
+// (row kd leaves).  No R_A, no LDS round trip or lds_sync per rotation.  B's rows keep explicit
+// zeros left of the diagonal, and the sweep writes those zeros too.
+template <class Mark>
+__device__ __forceinline__ void gi16_drop_b(GIState<16>& S, RegFactors& F, int kd, const Mark& mark) {
+  const int lane = qlane(), i = lane & 15;
+  const int q = S.q;
+  double* sB = F.sB;
+  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
+  mark(S, idk, false);
+  lds_sync();  // B's columns written by the adds
+  {
+    const double un = lane_next<16>(S.uw);
+    const int wn = lane_next_i<16>(S.ww);
+    if (i >= kd && i < q - 1) {
+      S.uw = un;
+      S.ww = wn;
+    }
+  }
+  // rotation jj's parameters on lane jj (every row block computes the same)
+  const double y = (i >= kd && i < q) ? sB[kd * kBS + i] : 0.0;
+  const double s2 = block_prefix<16>(y * y, i, 16, true, nullptr);  // |B(kd, kd..i)|^2
+  const double yn = lane_next<16>(y), r2 = lane_next<16>(s2);
+  double cs = 1.0, sn = 0.0;
+  if (i >= kd && i < q - 1 && r2 > 0.0) {
+    const double x = i == kd ? y : (s2 > 0.0 ? s2 * rsq_nr(s2) : 0.0);
+    const double ri = rsq_nr(r2);
+    cs = yn * ri;
+    sn = -x * ri;
+  }
+  double cb = lane < q ? sB[lane * kBS + kd] : 0.0;
+  const int wdst = lane > kd ? lane - 1 : lane;
+#pragma nounroll
+  for (int jj = kd; jj < q - 1; ++jj) {
+    const double c = bcast(cs, jj), sg = bcast(sn, jj);
+    rb_rotate_cols(F.J, jj, c, sg);
+    const double nb = lane < q ? sB[lane * kBS + jj + 1] : 0.0;
+    if (lane < q && lane != kd) sB[wdst * kBS + jj] = c * cb + sg * nb;
+    cb = -sg * cb + c * nb;
+    S.nrot += 1;
+  }
+  const int qn = q - 1;
+  if (i == qn) {
+    S.uw = 0.0;
+    S.ww = -1;
+  }
+  S.q = qn;
+  lds_sync();
+}
+
 // the QP of one step (M <= 16): unconstrained minimiser xu (row vector), u(t-1) of the row's MV
 // up_row, the row's constraint data rc (both replicated over the four row blocks); the optimal
 // moves come back in xout (row vector, registers; xu itself when it is feasible).  rebuild: the
 // J rebuild interval in units of M rotations (gpc_qp.h); PACKED: R^-1's layout (rinv_idx)
-template <bool PACKED = false>
+template <bool PACKED = false, class PAcc = void>
 __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, int Nu,
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
                                        int* st, GIState<16>& S, RegFactors& F, int rebuild, double& xout
 #ifdef MPCT_PROFILE
-                                       , ProfAcc& pacc, unsigned long long& pprev
+                                       , PAcc& pacc, unsigned long long& pprev
 #endif
                                        ) {
   const int lane = qlane(), i = lane & 15;
@@ -460,7 +521,8 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
 #ifdef MPCT_PROFILE
         pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
 #endif
-        gi16_drop(S, F, sRA, M, kd, mark);
+        if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kd, mark);
+        else gi16_drop(S, F, sRA, M, kd, mark);
         {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
           const double cn = lane_next<16>(c);
           if (i >= kd && i < q - 1) c = cn;
@@ -542,7 +604,8 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
 #ifdef MPCT_PROFILE
       pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kdrop) * kProfCount;
 #endif
-      gi16_drop(S, F, sRA, M, kdrop, mark);
+      if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kdrop, mark);
+      else gi16_drop(S, F, sRA, M, kdrop, mark);
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;

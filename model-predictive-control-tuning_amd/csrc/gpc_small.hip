@@ -72,6 +72,9 @@ __device__ __forceinline__ int sm_lane() {
 // LDS, so 16 workgroups fit a CU and the metric's 4096 simulations run in one round.  Against three
 // waves: bitwise the same results, 3.11-3.19 against 3.38-3.46 ms at 8192 candidates, the same
 // 2.21-2.24 ms at 4096 (profiles/r04b_small_ab.txt)
+#ifndef MPCT_SM_EARLY_XS
+#define MPCT_SM_EARLY_XS 1
+#endif
 __global__ void __launch_bounds__(64, 4)
     gpc_small_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
                      const int* __restrict__ Nuv, const double* __restrict__ deltav,
@@ -167,6 +170,11 @@ __global__ void __launch_bounds__(64, 4)
     lds_sync();  // rings of step t - 1 -> this step's plant terms and product
     // ---- plant (exact difference equations of every entry, lsim)
     const double hv = lds[pbase + ((t - pc) & pmask)];
+#if MPCT_SM_EARLY_XS
+    // the y update's reads of its own state (step t - 1's nabla y, nabla^2 y), issued with the ring
+    // read so that their latency hides under the plant's reductions (every lane reads a valid slot)
+    const double o1e = lds[L.xy + yoff + 1], o2e = lds[L.xy + yoff + 2];
+#endif
     const double ye = row4_sum(pcoef * hv);  // y_e(t) on lane e of every row
     double yi = ye + dppd<kQx1>(ye);
     yi += dppd<kQx2>(yi);  // y_i(t) on every lane of quad i
@@ -179,7 +187,11 @@ __global__ void __launch_bounds__(64, 4)
         // nabla^1,2 y(t-1) are the state's own entries of the last step (read before they are
         // overwritten); y(t-1) stays in a register
         double* xs = lds + L.xy + yoff;
+#if MPCT_SM_EARLY_XS
+        const double o1 = o1e, o2 = o2e;
+#else
         const double o1 = xs[1], o2 = xs[2];
+#endif
         const double n1 = yi - yd0, n2 = n1 - o1, n3 = n2 - o2;
         xs[0] = yi - r_t;
         if (nyh > 1) xs[1] = n1;

@@ -58,16 +58,29 @@ constexpr double kRelTol = MPCT_BAND_RELTOL;
 #define MPCT_BAND_RN_F64 0
 #endif
 typedef std::conditional_t<MPCT_BAND_RN_F64 != 0, double, float> rn_t;
-// the widest class (Mz > 32, MAXM = 64) keeps B = R_A^-1 instead of R_A, in R_A's packed place
-// (band_drop_b): the dual direction r = R_A^-1 d, the warm start's R_A'w = c and lambda = R_A^-1 w
+// every class keeps B = R_A^-1 instead of R_A, in R_A's packed place (band_drop_b): the dual direction r = R_A^-1 d, the warm start's R_A'w = c and lambda = R_A^-1 w
 // become products over the active set instead of serial substitutions (one broadcast per active
 // constraint, q ~ 41 on config 3's slowest simulations), and a drop's rotations come from B's row
 // instead of a chain of LDS round trips through R_A.  MPCT_BAND_EXB=0 keeps R_A in every class
 #ifndef MPCT_BAND_EXB
 #define MPCT_BAND_EXB 1
 #endif
+// the classes that keep B (MAXM, bits: 16 -> 1, 32 -> 2, 64 -> 4).  Config-3 grid: 64 only 0.913 s,
+// 32 and 64 0.897 s, all three 0.894 s (gpurun_out/r05k)
+#ifndef MPCT_BAND_EXB_CLASSES
+#define MPCT_BAND_EXB_CLASSES 7
+#endif
 
 namespace mpct {
+
+// J's column stride.  MPCT_BAND_LDJ_ODD=1 pads it to an odd count, so that dvec's reads (lane k
+// walks column k of JT) fall in distinct LDS banks for 32 lanes (config 3's Mz = 46 and 10 are
+// even).  The kernel's LDS bank conflicts are 4.6 % of its LDS cycles (profiles/r05_sq_workloads.json)
+// and the padding measured 0.912 / 0.913 s against 0.895 / 0.896 s for the grid (gpurun_out/r05o)
+#ifndef MPCT_BAND_LDJ_ODD
+#define MPCT_BAND_LDJ_ODD 0
+#endif
+__host__ __device__ constexpr int band_ldj(int Mz) { return MPCT_BAND_LDJ_ODD ? (Mz | 1) : Mz; }
 
 struct BandLayout {
   int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, rn, plb, pla,
@@ -101,8 +114,8 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.ri = take(full_ri ? Mz * Mz : Mz);
-  L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
-  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked); B = R_A^-1 there when MAXM = 64
+  L.jt = take(Mz * band_ldj(Mz));  // J, column-major JT[k*ldj + i] = J(i,k) (R parks here, stride Mz)
+  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked), or B = R_A^-1 in its place (band_drop_b)
   L.dv = take(Mz);       // d = J'n
   L.nv = take(Mz);       // staged normal n_p
   L.xc = take(Mz);       // QP iterate
@@ -135,7 +148,7 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   return L;
 }
 
-// B = R_A^-1 of the band kernel's widest class, in R_A's packed layout (gi_core.h RAPacked: column
+// B = R_A^-1 of the band kernel, in R_A's packed layout (gi_core.h RAPacked: column
 // k holds rows 0..k+1).  Entry (k + 1, k) is kept zero on the active block, and bt_mul / bt_tmul
 // read it in place of every entry below the stored ones.
 __device__ __forceinline__ int bt_idx(int w, int k) { return (int)(__umul24((unsigned)k, (unsigned)(k + 3)) >> 1) + w; }
@@ -218,16 +231,16 @@ __device__ __forceinline__ double wave_prefix_sum(double v) {
 // through them with the running entry in a register, writing B's rows kd + 1.. one row up.
 // The same factorisation as the R_A form up to the signs of R_new's rows (Givens QR is unique up
 // to them), which J and B carry consistently.  cs / sn are staged in sc_ / ss_ (Mz doubles each).
-template <class Mark>
-__device__ __forceinline__ void band_drop_b(GIState<64>& S, double* sJT, double* bt, int Mz, int kd,
+template <int MAXM, class Mark>
+__device__ __forceinline__ void band_drop_b(GIState<MAXM>& S, double* sJT, double* bt, int Mz, int ldj, int kd,
                                             const Mark& mark, double* sc_, double* ss_) {
   const int lane = threadIdx.x;
   const int q = S.q;
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);
   {
-    const double un = lane_next<64>(S.uw);
-    const int wn = lane_next_i<64>(S.ww);
+    const double un = lane_next<MAXM>(S.uw);
+    const int wn = lane_next_i<MAXM>(S.ww);
     if (lane >= kd && lane < q - 1) {
       S.uw = un;
       S.ww = wn;
@@ -236,7 +249,7 @@ __device__ __forceinline__ void band_drop_b(GIState<64>& S, double* sJT, double*
   // rotation parameters: lane jj in [kd, q-2]
   const double y = (lane >= kd && lane < q) ? bt[bt_idx(kd, lane)] : 0.0;
   const double s2 = wave_prefix_sum(y * y);  // lane j: |B(kd, kd..j)|^2
-  const double yn = lane_next<64>(y), r2 = lane_next<64>(s2);
+  const double yn = lane_next<MAXM>(y), r2 = lane_next<MAXM>(s2);
   if (lane >= kd && lane < q - 1) {
     const double x = lane == kd ? y : (s2 > 0.0 ? s2 * rsq_nr(s2) : 0.0);
     double cs = 1.0, sn = 0.0;
@@ -251,20 +264,20 @@ __device__ __forceinline__ void band_drop_b(GIState<64>& S, double* sJT, double*
   lds_sync();
   // J's columns (lanes = rows of J) and B's rows by slot (lanes = rows w < q)
   const bool jrow = lane < Mz, brow = lane < q;
-  double cj = jrow ? sJT[kd * Mz + lane] : 0.0;
+  double cj = jrow ? sJT[kd * ldj + lane] : 0.0;
   double cb = (brow && lane <= kd + 1) ? bt[bt_idx(lane, kd)] : 0.0;
   const int wdst = lane > kd ? lane - 1 : lane;  // B's row kd leaves: rows below move up one
   for (int jj = kd; jj < q - 1; ++jj) {
     const double cs = sc_[jj], sn = ss_[jj];
-    const double nj = jrow ? sJT[(jj + 1) * Mz + lane] : 0.0;
+    const double nj = jrow ? sJT[(jj + 1) * ldj + lane] : 0.0;
     const double nb = (brow && lane <= jj + 2) ? bt[bt_idx(min(lane, jj + 2), jj + 1)] : 0.0;
-    if (jrow) sJT[jj * Mz + lane] = cs * cj + sn * nj;
+    if (jrow) sJT[jj * ldj + lane] = cs * cj + sn * nj;
     const double vb = cs * cb + sn * nb;
     if (brow && lane != kd && wdst <= jj + 1) bt[bt_idx(wdst, jj)] = vb;
     cj = -sn * cj + cs * nj;
     cb = -sn * cb + cs * nb;
   }
-  if (jrow) sJT[(q - 1) * Mz + lane] = cj;
+  if (jrow) sJT[(q - 1) * ldj + lane] = cj;
   const int qn = q - 1;
   if (lane == qn) {
     S.uw = 0.0;
@@ -310,7 +323,7 @@ __global__ void __launch_bounds__(64, 1)
   const int P = my * N2;
   int st = 0;
 #ifdef MPCT_PROFILE
-  ProfAcc pacc;
+  ProfAccS pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -349,9 +362,10 @@ __global__ void __launch_bounds__(64, 1)
   const int tls = sc.tlen;
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
+  const int ldj = band_ldj(Mz);
   double* sRA = lds + L.ra;
   const RAPacked rap{};
-  constexpr bool EXB = MPCT_BAND_EXB != 0 && MAXM == 64;  // B = R_A^-1 in R_A's place (band_drop_b)
+  constexpr bool EXB = MPCT_BAND_EXB != 0 && ((MPCT_BAND_EXB_CLASSES >> (MAXM == 64 ? 2 : MAXM == 32 ? 1 : 0)) & 1);
   double* sBT = lds + L.ra;
   double* sd = lds + L.dv;
   double* snv = lds + L.nv;
@@ -526,11 +540,11 @@ __global__ void __launch_bounds__(64, 1)
   // J = R^-1 (gi_load_rinv), or its diagonal in band mode
   auto load_j = [&]() __attribute__((always_inline)) {
     if (any_q) {
-      gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
+      gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row, ldj);
     } else {
       if (row) {
         const double dj = sRi[lane];
-        for (int k = 0; k < Mz; ++k) sJT[k * Mz + lane] = k == lane ? dj : 0.0;
+        for (int k = 0; k < Mz; ++k) sJT[k * ldj + lane] = k == lane ? dj : 0.0;
       }
       gis.nrot = 0;
       gis.jinit = true;
@@ -600,7 +614,7 @@ __global__ void __launch_bounds__(64, 1)
     lds_sync();
     double dk = 0.0;
     if (row) {
-      const double* jc = sJT + lane * Mz;
+      const double* jc = sJT + lane * ldj;
       double d1 = 0.0;
       int r = 0;
       for (; r + 3 < Mz; r += 4) {  // four terms' loads together, the two-term loop's order
@@ -765,13 +779,13 @@ __global__ void __launch_bounds__(64, 1)
           const double dk = dvec(p);
           const double beta = qsum<MAXM>(lane >= v && row ? dk * dk : 0.0);
           lds_sync();
-          const double zm = gi_z(sJT, sd, v, Mz, row);
+          const double zm = gi_z(sJT, sd, v, Mz, row, ldj);
           const double uk = gis.uw;
           if constexpr (EXB)
             gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, RANone{},
-                         BandBAdd{sBT, bt_mul(sBT, sd, v)});
+                         BandBAdd{sBT, bt_mul(sBT, sd, v)}, ldj);
           else
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap);
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap, GINoExt{}, ldj);
           if (lane == v) gis.uw = uk;
           ++it;
         }
@@ -807,10 +821,10 @@ __global__ void __launch_bounds__(64, 1)
             double x1 = 0.0;
             int v = 0;
             for (; v + 1 < q; v += 2) {
-              x = fma(sJT[v * Mz + lane], sd[v], x);
-              x1 = fma(sJT[(v + 1) * Mz + lane], sd[v + 1], x1);
+              x = fma(sJT[v * ldj + lane], sd[v], x);
+              x1 = fma(sJT[(v + 1) * ldj + lane], sd[v + 1], x1);
             }
-            if (v < q) x = fma(sJT[v * Mz + lane], sd[v], x);
+            if (v < q) x = fma(sJT[v * ldj + lane], sd[v], x);
             x += x1;
           }
           lam = bt_mul(sBT, sd, q);
@@ -821,7 +835,7 @@ __global__ void __launch_bounds__(64, 1)
           double ra = lane < Mz ? sRA[rap(0, lane)] : 0.0, jv = row ? sJT[lane] : 0.0;
           for (int v = 0; v < q; ++v) {
             const int vn = v + 1 < q ? v + 1 : v;
-            const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * Mz + lane] : 0.0;
+            const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * ldj + lane] : 0.0;
             const double w = bcast(cc * gis.rdg, v);
             if (lane == v) wv = w;
             if (lane > v && lane < q) cc -= ra * w;
@@ -836,8 +850,8 @@ __global__ void __launch_bounds__(64, 1)
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, kd, mark, snv, sd);
-        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap);
+        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, ldj, kd, mark, snv, sd);
+        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap, GINoExt{}, ldj);
         ++it;
       }
       return row ? x : 0.0;
@@ -908,7 +922,7 @@ __global__ void __launch_bounds__(64, 1)
         const double dn2 = qsum<MAXM>(d2);
         const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
         lds_sync();
-        const double zm = gi_z(sJT, sd, gis.q, Mz, row);
+        const double zm = gi_z(sJT, sd, gis.q, Mz, row, ldj);
         PSTAMP(PROF_QD);
         double rk;
         if constexpr (EXB) rk = bt_mul(sBT, sd, gis.q);
@@ -935,14 +949,14 @@ __global__ void __launch_bounds__(64, 1)
         sp += t * beta;
         if (full) {
           if constexpr (EXB)
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk});
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk}, ldj);
           else
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap);
+            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap, GINoExt{}, ldj);
           PSTAMP(PROF_QADD);
           break;
         }
-        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, kdrop, mark, snv, sd);
-        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap);
+        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, ldj, kdrop, mark, snv, sd);
+        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap, GINoExt{}, ldj);
         PSTAMP(PROF_QDROP);
         if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64, 1)
   int st = 0;
 #ifdef MPCT_PROFILE
   // diagnostic build: section cycle sums (tools/nmpc_latency.py --profile; labels: mpct_host.cpp)
-  ProfAcc pacc;
+  ProfAccS pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
 #endif
 

@@ -311,9 +311,17 @@ __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
 // diagnostic build: section k's cycles in the low 48 bits of pacc[k], the number of times the
 // section ended in the high 16 (tools/latency_model.py divides one by the other)
 constexpr unsigned long long kProfCount = 1ull << 48;
-// the section words live in one 64-bit VGPR pair, lane k holding word k: an SGPR array of PROF_N
-// words (the first form) was copied whole at every loop back-edge of the step loop (28 s_mov per
-// QP iteration), which inflated the sections it was measuring
+// ProfAcc: the section words live in one 64-bit VGPR pair, lane k holding word k.  The SGPR array
+// of PROF_N words (ProfAccS, the first form) was copied whole at every loop back-edge of the metric
+// kernel's step loop (28 s_mov per QP iteration), which inflated the sections it was measuring.
+// A VALU add lands only in active lanes, so ProfAcc needs every stamp at a wave-uniform point (the
+// metric kernel's are); the band, NMPC and general kernels stamp inside lane-divergent code and
+// keep ProfAccS
+struct ProfAccS {
+  unsigned long long w[PROF_N] = {};
+  __device__ __forceinline__ unsigned long long& operator[](int k) { return w[k]; }
+  __device__ __forceinline__ unsigned long long get(int k) const { return w[k]; }
+};
 struct ProfAcc {
   unsigned long long v = 0;
   struct Ref {
