@@ -53,6 +53,13 @@ constexpr int kBS = 16;
 // 1: drops from B alone (gi16_drop_b), no R_A kept; 0: R_A in LDS and its Givens chain (gi16_drop).
 // Measured the same at 4096 candidates and 1 % slower on the heaviest 256 (gpurun_out/r05l): the
 // metric's drops average three rotations, and J's register rotations dominate them either way
+// MPCT_QP16_WARM_DROPALL=1: the warm start drops every negative multiplier before re-solving,
+// instead of the most negative one.  More drops and re-adds follow (608k -> 733k QP iterations on
+// the 4096 grid) and the time is the same: 2.023 / 2.031 against 2.012 / 2.042 ms, heaviest 256
+// 1.840 / 1.846 against 1.838 / 1.839 ms (gpurun_out/r05p)
+#ifndef MPCT_QP16_WARM_DROPALL
+#define MPCT_QP16_WARM_DROPALL 0
+#endif
 #ifndef MPCT_QP16_BDROP
 #define MPCT_QP16_BDROP 0
 #endif
@@ -514,6 +521,26 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         const double lam = row4_sum(la);
 #endif
         if (i < q) S.uw = lam;
+#if MPCT_QP16_WARM_DROPALL
+        // every constraint with a negative multiplier leaves before the next solve (highest index
+        // first, so the lower ones keep their lanes); the one-at-a-time form re-solves after each
+        unsigned long long neg = __ballot(i < q && lam < 0.0) & 0xFFFFull;
+        if (neg == 0) break;
+        while (neg) {
+          const int kd = 63 - __builtin_clzll(neg);
+          neg &= ~(1ull << kd);
+          const int qd = S.q;
+#ifdef MPCT_PROFILE
+          pacc[PROF_QROT] += (unsigned long long)(qd - 1 - kd) * kProfCount;
+#endif
+          if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kd, mark);
+          else gi16_drop(S, F, sRA, M, kd, mark);
+          const double cn = lane_next<16>(c);  // c follows the ids
+          if (i >= kd && i < qd - 1) c = cn;
+          else if (i == qd - 1) c = 0.0;
+          ++it;
+        }
+#else
         double lmin = i < q ? lam : INFINITY;
         int kd = i;
         qargmin<16>(lmin, kd, 0);
@@ -529,6 +556,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
           else if (i == q - 1) c = 0.0;
         }
         ++it;
+#endif
       }
       if (!row) xm = 0.0;
     }

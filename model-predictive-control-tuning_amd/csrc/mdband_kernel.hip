@@ -77,6 +77,12 @@ namespace mpct {
 // walks column k of JT) fall in distinct LDS banks for 32 lanes (config 3's Mz = 46 and 10 are
 // even).  The kernel's LDS bank conflicts are 4.6 % of its LDS cycles (profiles/r05_sq_workloads.json)
 // and the padding measured 0.912 / 0.913 s against 0.895 / 0.896 s for the grid (gpurun_out/r05o)
+// MPCT_BAND_STEP_LDS=1: the QP's step rows copied to LDS when they fit the simulation's tier
+// (band_layout).  Bitwise the same results; grid 0.922 / 0.923 s against 0.925 / 0.927 s, slowest
+// simulation 116 against 117 ms (gpurun_out/r05p): within noise, so the QP reads L1 / L2
+#ifndef MPCT_BAND_STEP_LDS
+#define MPCT_BAND_STEP_LDS 0
+#endif
 #ifndef MPCT_BAND_LDJ_ODD
 #define MPCT_BAND_LDJ_ODD 0
 #endif
@@ -86,6 +92,7 @@ struct BandLayout {
   int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, rn, plb, pla,
       mzb, mza, total;
   int yh, ur, ts;  // entry output ring, input ring (powers of two) and tail stride of this scenario
+  int stq;         // the QP's copy of the step rows (s_in(0..N2)), or -1 (band_layout)
 };
 
 __host__ __device__ inline int pow2_at_least(int n) {
@@ -145,6 +152,23 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.mzb = take(ne * sc.mz_maxbc);
   L.mza = take(ne * sc.mz_maxa);
   L.total = (o + 1) & ~1;
+  // the step rows s_in(0..N2) the QP reads in every output-row scan (yhat) and normal (dvec), copied
+  // to LDS when they fit under the LDS tier the simulation occupies anyway (the same values: bitwise
+  // the same results); otherwise the QP reads the scenario's table through L1 / L2
+  L.stq = -1;
+  if (MPCT_BAND_STEP_LDS) {
+    const int nq = (my * nu * (N2 + 1) + 1) & ~1;
+    long long cap = 0;
+    for (long long c : kBandCapsKb)
+      if (c * 1024 >= (long long)L.total * 8) {
+        cap = c * 1024;
+        break;
+      }
+    if (cap && (long long)(L.total + nq) * 8 <= cap) {
+      L.stq = L.total;
+      L.total += nq;
+    }
+  }
   return L;
 }
 
@@ -389,6 +413,9 @@ __global__ void __launch_bounds__(64, 1)
   double* smzb = lds + L.mzb;
   double* smza = lds + L.mza;
   const double* __restrict__ sstep = sc.step;  // global, L1/L2-resident
+  const bool stq = L.stq >= 0;                  // the QP's LDS copy of the step rows (band_layout)
+  const double* sstq = stq ? lds + L.stq : sstep;
+  const int tlq = stq ? N2 + 1 : sc.tlen;
 
   // ------------------------------------------------------------------ prologue
   for (int e = lane; e < ne * sc.pl_maxbc; e += kWave) {
@@ -402,6 +429,11 @@ __global__ void __launch_bounds__(64, 1)
   }
   for (int e = lane; e < ne * sc.mz_maxa; e += kWave) smza[e] = sc.mz_a[e];
   for (int e = lane; e < 4 * my; e += kWave) sob[e] = sc.obnd[e];
+  if (stq)
+    for (int e = lane; e < my * nu * (N2 + 1); e += kWave) {
+      const int in = e / (N2 + 1), t = e - in * (N2 + 1);
+      lds[L.stq + e] = sstep[in * sc.tlen + t];
+    }
   for (int e = lane; e < L.plb - L.fr; e += kWave) lds[L.fr + e] = 0.0;
   const bool row = lane < Mz;  // QP-row lanes: moves 0..M-1, eps at M
   RowCons rcn;
@@ -557,7 +589,7 @@ __global__ void __launch_bounds__(64, 1)
     double a0 = F[g], a1 = 0.0;
     const int lmax = min(Nu - 1, k + 1);
     for (int n = 0; n < nu; ++n) {
-      const double* sp = sstep + (i * nu + n) * tls + (k + 1);
+      const double* sp = sstq + (i * nu + n) * tlq + (k + 1);
       const double* xp = sxc + n * Nu;
       int l = 0;
       // four taps per trip, their loads issued together; the accumulation order (even taps into
@@ -603,7 +635,7 @@ __global__ void __launch_bounds__(64, 1)
         const int q = p - base, g = q >> 1, i = g / N2, k = g - i * N2;
         if (lane < M) {
           const int tt = k + 1 - rcn.l;
-          nvv = tt >= 0 ? sstep[(i * nu + rcn.n) * tls + tt] : 0.0;
+          nvv = tt >= 0 ? sstq[(i * nu + rcn.n) * tlq + tt] : 0.0;
           if (!(q & 1)) nvv = -nvv;
         } else {
           nvv = sob[((q & 1) ? 2 : 3) * my + i];
@@ -1213,8 +1245,11 @@ __global__ void __launch_bounds__(64, 1)
 namespace mpct {
 
 long long mdband_lds_bytes(const DevScenario& sc, int N2, int Nu, int ncopy) {
-  const BandLayout L = band_layout(sc, N2, sc.nu * Nu, true, ncopy);
-  return (long long)L.total * 8;
+  // the larger of the two R^-1 forms (full triangle / band-mode diagonal): the step-row copy of
+  // band_layout depends on the rest of the layout, so neither total bounds the other
+  const BandLayout Lf = band_layout(sc, N2, sc.nu * Nu, true, ncopy);
+  const BandLayout Ld = band_layout(sc, N2, sc.nu * Nu, false, ncopy);
+  return (long long)std::max(Lf.total, Ld.total) * 8;
 }
 
 // One launch per (QP size class MAXM, occupancy class): the dynamic LDS of a launch is what its

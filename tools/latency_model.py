@@ -50,15 +50,15 @@ CHAINS = {
     "qp(rest)": {"block_prefix16_nu5": 1, "add_f64": 4, "ballot_branch": 1},
     # the first move by ds_bpermute from the QP's register result, u = u(t-1) + du, ring store (:234-247)
     "u_update": {"shfl_bpermute": 1, "add_f64": 1},
-    # most violated inactive constraint: slacks at x, the min over the lane's four kinds, the packed-
-    # key DPP argmin, the winner's value by readlane, the branch (gpc_qp16.h:445-461)
-    "qp.check": {"block_prefix16_nu5": 1, "add_f64": 4, "qargmin16_key": 1, "uniform_branch": 1},
+    # most violated inactive constraint: slacks at x, the min over the lane's four kinds, the exact
+    # 16-lane argmin and its lane-0 broadcast (wave_ops.h qargmin), the branch (gpc_qp16.h)
+    "qp.check": {"block_prefix16_nu5": 1, "add_f64": 4, "qargmin16_exact": 1, "uniform_branch": 1},
     # d = J'n_p (row16 DPP sum, four chains side by side), the products' d^2 FOR4 chain and one
     # permlane row4 sum (the five run side by side) (gpc_qp16.h:192-225, :478-484)
     "qp.d+z": {"row_sum16": 1, "mul_f64": 2, "add_f64": 4, "row4_sum_permlane": 1},
-    # ratio test: qp_div (rcp + Newton), the packed-key argmin, t2 beside it, two uniform branches,
+    # ratio test: qp_div (rcp + Newton), the exact argmin, t2 beside it, two uniform branches,
     # x += t z (gpc_qp16.h:485-506)
-    "qp.r+t1": {"rcp_nr": 1, "mul_f64": 1, "qargmin16_key": 1, "uniform_branch": 2, "fma_f64": 1},
+    "qp.r+t1": {"rcp_nr": 1, "mul_f64": 1, "qargmin16_exact": 1, "uniform_branch": 2, "fma_f64": 1},
     # add: d_q by readlane, |d(q:)| by rsq, 2/v'v by rcp, the J column update, B / R_A columns to LDS,
     # lds_sync before the next read (gpc_qp16.h:229-263)
     "qp.add": {"bcast_readlane": 1, "rsq_nr": 1, "fma_f64": 2, "rcp_nr": 1, "mul_f64": 1, "lds_handoff": 1},
@@ -67,10 +67,10 @@ CHAINS = {
     # priced per drop with one rotation (the counted rotations add per rotation below)
     "qp.drop": {"bcast_readlane": 1, "lds_handoff": 3, "dpp_stage_f64": 1},
     # warm start: the slacks' gather by ds_bpermute, w = B'c (row16 DPP), x = x_u + J w and
-    # lambda = B w (FOR4 chains + permlane row4 sums), the multipliers' packed-key argmin, the
+    # lambda = B w (FOR4 chains + permlane row4 sums), the multipliers' exact argmin, the
     # branch (gpc_qp16.h:396-440); per pass of its loop
     "qp.warm": {"shfl_bpermute": 1, "mul_f64": 1, "row_sum16": 1, "fma_f64": 4, "row4_sum_permlane": 1,
-                "add_f64": 1, "qargmin16_key": 1, "uniform_branch": 1},
+                "add_f64": 1, "qargmin16_exact": 1, "uniform_branch": 1},
 }
 # one Givens rotation of the drop: entries read, a^2 + b^2, rsq + Newton, cs / sn, the RMW of R_A's
 # two rows, lds_sync (gpc_qp16.h:289-310)

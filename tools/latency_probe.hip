@@ -4,7 +4,7 @@
 // the metric kernel, tools/latency_model.py).  Each probe repeats one dependent step kRep times per
 // trip and kTrips trips; cycles per step = (stamp difference) / (kRep * kTrips), minus nothing: the
 // loop overhead is one SALU compare and branch per kRep steps.  Built by hand (not part of build()):
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I model-predictive-control-tuning_amd/csrc \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMPCT_PACKED_ARGMIN=1 -I model-predictive-control-tuning_amd/csrc \
 //         tools/latency_probe.hip -o tools/latency_probe
 // Usage: tools/latency_probe  -> one JSON object {probe: cycles per step}
 #include <hip/hip_runtime.h>
