@@ -80,6 +80,11 @@ namespace mpct {
 // MPCT_BAND_STEP_LDS=1: the QP's step rows copied to LDS when they fit the simulation's tier
 // (band_layout).  Bitwise the same results; grid 0.922 / 0.923 s against 0.925 / 0.927 s, slowest
 // simulation 116 against 117 ms (gpurun_out/r05p): within noise, so the QP reads L1 / L2
+// MPCT_BAND_YHAT8=1: the scan's prediction takes eight taps per trip.  Bitwise the same; grid
+// 0.908 / 0.910 against 0.895 / 0.897 s, slowest simulation unchanged (gpurun_out/r05r): not kept
+#ifndef MPCT_BAND_YHAT8
+#define MPCT_BAND_YHAT8 0
+#endif
 #ifndef MPCT_BAND_STEP_LDS
 #define MPCT_BAND_STEP_LDS 0
 #endif
@@ -592,6 +597,22 @@ __global__ void __launch_bounds__(64, 1)
       const double* sp = sstq + (i * nu + n) * tlq + (k + 1);
       const double* xp = sxc + n * Nu;
       int l = 0;
+#if MPCT_BAND_YHAT8
+      for (; l + 7 <= lmax; l += 8) {  // eight taps' loads in flight, the same accumulation order
+        const double s0 = sp[-l], s1 = sp[-l - 1], s2 = sp[-l - 2], s3 = sp[-l - 3];
+        const double s4 = sp[-l - 4], s5 = sp[-l - 5], s6 = sp[-l - 6], s7 = sp[-l - 7];
+        const double x0 = xp[l], x1 = xp[l + 1], x2 = xp[l + 2], x3 = xp[l + 3];
+        const double x4 = xp[l + 4], x5 = xp[l + 5], x6 = xp[l + 6], x7 = xp[l + 7];
+        a0 += s0 * x0;
+        a1 += s1 * x1;
+        a0 += s2 * x2;
+        a1 += s3 * x3;
+        a0 += s4 * x4;
+        a1 += s5 * x5;
+        a0 += s6 * x6;
+        a1 += s7 * x7;
+      }
+#endif
       // four taps per trip, their loads issued together; the accumulation order (even taps into
       // a0, odd into a1) is the two-tap loop's
       for (; l + 3 <= lmax; l += 4) {
