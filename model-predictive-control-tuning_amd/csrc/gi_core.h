@@ -79,15 +79,14 @@ __device__ __forceinline__ void gi_reset(GIState<MAXM>& S) {
 
 template <int MAXM>
 __device__ __forceinline__ void gi_load_rinv(GIState<MAXM>& S, double* sJT, const double* sRi, int M,
-                                             bool row, int ld = 0) {  // ld: J's column stride (0: M)
+                                             bool row) {
   const int lane = qp_lane();
-  const int LD = ld ? ld : M;
   // not unrolled: the x8 unroll hoists eight strided LDS pointers, the one VGPR over the 3-wave
   // budget of gpc_closed_loop_kernel<16>, spilled to scratch (~1 MiB of write-backs per metric
   // launch); the rebuild runs once per 32 updates so the loop overhead is noise
   if (row)
 #pragma unroll 1
-    for (int k = 0; k < M; ++k) sJT[k * LD + lane] = sRi[lane * M + k];
+    for (int k = 0; k < M; ++k) sJT[k * M + lane] = sRi[lane * M + k];
   S.nrot = 0;
   S.jinit = true;
   lds_sync();
@@ -108,15 +107,14 @@ __device__ __forceinline__ double gi_dvec(const double* sJT, double* sd, int M, 
 }
 
 // z_i = sum_{k >= q} J(i,k) d_k  (d in sd, synchronised by the caller)
-__device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row, int ld = 0) {
+__device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int q, int M, bool row) {
   const int lane = qp_lane();
-  const int LD = ld ? ld : M;
   double z0 = 0.0, z1 = 0.0;
   if (row) {
     int k = q;
     for (; k + 3 < M; k += 4) {  // four terms' loads together, the two-term loop's order
-      const double j0 = sJT[k * LD + lane], j1 = sJT[(k + 1) * LD + lane];
-      const double j2 = sJT[(k + 2) * LD + lane], j3 = sJT[(k + 3) * LD + lane];
+      const double j0 = sJT[k * M + lane], j1 = sJT[(k + 1) * M + lane];
+      const double j2 = sJT[(k + 2) * M + lane], j3 = sJT[(k + 3) * M + lane];
       const double d0 = sd[k], d1 = sd[k + 1], d2 = sd[k + 2], d3 = sd[k + 3];
       z0 += j0 * d0;
       z1 += j1 * d1;
@@ -124,10 +122,10 @@ __device__ __forceinline__ double gi_z(const double* sJT, const double* sd, int 
       z1 += j3 * d3;
     }
     for (; k + 1 < M; k += 2) {
-      z0 += sJT[k * LD + lane] * sd[k];
-      z1 += sJT[(k + 1) * LD + lane] * sd[k + 1];
+      z0 += sJT[k * M + lane] * sd[k];
+      z1 += sJT[(k + 1) * M + lane] * sd[k + 1];
     }
-    if (k < M) z0 += sJT[k * LD + lane] * sd[k];
+    if (k < M) z0 += sJT[k * M + lane] * sd[k];
   }
   return z0 + z1;
 }
@@ -184,44 +182,39 @@ __device__ __forceinline__ double gi_backsub(const GIState<MAXM>& S, const doubl
   return gi_backsub<MAXM>(S, sRA, M, c, RAFull{M});
 }
 
-// extra factors a caller keeps in step with R_A (the band kernel's explicit R_A^-1): gi_add calls
-// add(q, 1 / alpha) for the new column q, gi_drop calls rot(jj, q, cs, sn) with every Givens
-// rotation of R_A's rows (jj, jj + 1) and drop_rows(kd, q) after the last one, each before the
-// lds_sync that ends the step
+// an extra factor a caller keeps in step with the active set (the band kernel's B = R_A^-1):
+// gi_add calls add(q, 1 / alpha) for the new column q before the lds_sync that ends the add
 struct GINoExt {
   __device__ __forceinline__ void add(int, double) const {}
-  __device__ __forceinline__ void rot(int, int, double, double) const {}
-  __device__ __forceinline__ void drop_rows(int, int) const {}
 };
 
 // append constraint p (normal image d = J'n_p in dk / sd, beta = |d(q:)|^2, z = J(:,q:)d(q:))
 template <int MAXM, class Mark, class RAL, class Ext = GINoExt>
 __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sRA, const double* sd, int M,
                                        int p, double dk, double beta, double zm, double upm, bool row,
-                                       const Mark& mark, const RAL& ra, const Ext& ext = Ext{}, int ld = 0) {
+                                       const Mark& mark, const RAL& ra, const Ext& ext = Ext{}) {
   const int lane = qp_lane();
   const int q = S.q;
-  const int LD = ld ? ld : M;  // J's column stride
   const double dq = bcast(dk, q);
   const double nrm = beta * rsq_nr(beta);  // beta > 0 on an add
   const double alpha = dq > 0.0 ? -nrm : nrm;
   const double vq = dq - alpha;
   const double two_vtv = qp_rcp(beta - alpha * dq);  // 2 / v'v
   if (row) {
-    const double jq = sJT[q * LD + lane];
+    const double jq = sJT[q * M + lane];
     const double f = (zm - alpha * jq) * two_vtv;
-    sJT[q * LD + lane] = jq - f * vq;
+    sJT[q * M + lane] = jq - f * vq;
     int k = q + 1;
     for (; k + 3 < M; k += 4) {  // independent columns: four loads in flight
-      const double j0 = sJT[k * LD + lane], j1 = sJT[(k + 1) * LD + lane];
-      const double j2 = sJT[(k + 2) * LD + lane], j3 = sJT[(k + 3) * LD + lane];
+      const double j0 = sJT[k * M + lane], j1 = sJT[(k + 1) * M + lane];
+      const double j2 = sJT[(k + 2) * M + lane], j3 = sJT[(k + 3) * M + lane];
       const double d0 = sd[k], d1 = sd[k + 1], d2 = sd[k + 2], d3 = sd[k + 3];
-      sJT[k * LD + lane] = j0 - f * d0;
-      sJT[(k + 1) * LD + lane] = j1 - f * d1;
-      sJT[(k + 2) * LD + lane] = j2 - f * d2;
-      sJT[(k + 3) * LD + lane] = j3 - f * d3;
+      sJT[k * M + lane] = j0 - f * d0;
+      sJT[(k + 1) * M + lane] = j1 - f * d1;
+      sJT[(k + 2) * M + lane] = j2 - f * d2;
+      sJT[(k + 3) * M + lane] = j3 - f * d3;
     }
-    for (; k < M; ++k) sJT[k * LD + lane] -= f * sd[k];
+    for (; k < M; ++k) sJT[k * M + lane] -= f * sd[k];
   }
   if constexpr (RAL::store) {
     if (lane < q) sRA[ra(lane, q)] = dk;  // new column q of R_A = [d(0:q-1); alpha]
@@ -247,12 +240,11 @@ __device__ __forceinline__ void gi_add(GIState<MAXM>& S, double* sJT, double* sR
 }
 
 // remove active constraint kd: drop its column of R_A, re-triangularise with Givens on J
-template <int MAXM, class Mark, class RAL, class Ext = GINoExt>
+template <int MAXM, class Mark, class RAL>
 __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* sRA, int M, int kd,
-                                        const Mark& mark, const RAL& ra, const Ext& ext = Ext{}, int ld = 0) {
+                                        const Mark& mark, const RAL& ra) {
   const int lane = qp_lane();
   const int q = S.q;
-  const int LD = ld ? ld : M;  // J's column stride
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);
   if (lane < q) {  // remove column kd (lanes = rows; rows below w + 1 of the new column w are
@@ -283,17 +275,15 @@ __device__ __forceinline__ void gi_drop(GIState<MAXM>& S, double* sJT, double* s
           sRA[ra(jj + 1, lane)] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
         }
         if (lane < M) {
-          const double j0v = sJT[jj * LD + lane], j1v = sJT[(jj + 1) * LD + lane];
-          sJT[jj * LD + lane] = cs * j0v + sn * j1v;
-          sJT[(jj + 1) * LD + lane] = -sn * j0v + cs * j1v;
+          const double j0v = sJT[jj * M + lane], j1v = sJT[(jj + 1) * M + lane];
+          sJT[jj * M + lane] = cs * j0v + sn * j1v;
+          sJT[(jj + 1) * M + lane] = -sn * j0v + cs * j1v;
         }
-        ext.rot(jj, q, cs, sn);
         S.nrot += 1;
       }
       lds_sync();
     }
   }
-  ext.drop_rows(kd, q);
   const int qn = q - 1;
   if (lane == qn) {
     S.uw = 0.0;

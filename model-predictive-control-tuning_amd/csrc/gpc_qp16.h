@@ -50,19 +50,9 @@ struct RegFactors {
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
 // candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
 constexpr int kBS = 16;
-// 1: drops from B alone (gi16_drop_b), no R_A kept; 0: R_A in LDS and its Givens chain (gi16_drop).
-// Measured the same at 4096 candidates and 1 % slower on the heaviest 256 (gpurun_out/r05l): the
-// metric's drops average three rotations, and J's register rotations dominate them either way
-// MPCT_QP16_WARM_DROPALL=1: the warm start drops every negative multiplier before re-solving,
-// instead of the most negative one.  More drops and re-adds follow (608k -> 733k QP iterations on
-// the 4096 grid) and the time is the same: 2.023 / 2.031 against 2.012 / 2.042 ms, heaviest 256
-// 1.840 / 1.846 against 1.838 / 1.839 ms (gpurun_out/r05p)
-#ifndef MPCT_QP16_WARM_DROPALL
-#define MPCT_QP16_WARM_DROPALL 0
-#endif
-#ifndef MPCT_QP16_BDROP
-#define MPCT_QP16_BDROP 0
-#endif
+// Drops keep R_A and its Givens chain: drops derived from B alone, as the band kernel's (DESIGN §11
+// round 5), measured the same at 4096 candidates and 1 % slower on the heaviest 256 here (DESIGN §6
+// round 5): the metric's drops average three rotations, and J's register rotations dominate them
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
@@ -205,15 +195,9 @@ __device__ __forceinline__ void gi16_load_rinv(GIState<16>& S, RegFactors& F, co
 // d = J'n_p for constraint p (rows j0..mp of J, sign sg) -> column vector.  A one-row normal (the
 // rate rows, kinds 0/1) is row j0 of J itself: fetched by ds_bpermute (8 instructions) instead of
 // the 16-lane sum of the masked rows (48), the same value
-#ifndef MPCT_QP16_SUM4
-#define MPCT_QP16_SUM4 1
-#endif
-#ifndef MPCT_QP16_DVEC_BPERM
-#define MPCT_QP16_DVEC_BPERM 1
-#endif
 __device__ __forceinline__ void gi16_dvec(const RegFactors& F, int j0, int mp, double sg, d4v& d) {
   const int i = q16_i();
-  if (MPCT_QP16_DVEC_BPERM && j0 == mp) {
+  if (j0 == mp) {
     const int src = j0 + 16 * q16_b();
     FOR4(r, d[r] = __shfl(F.J[r], src, kWave););
   } else {
@@ -243,18 +227,11 @@ __device__ __forceinline__ void gi16_products(const RegFactors& F, const d4v& Bl
     }
   });
   const double jl = (b == (q >> 2)) ? sel4u(F.J, q & 3) : 0.0;
-#if MPCT_QP16_SUM4
   z = za;
   jq = jl;
   rk = ra;
   dn2 = s1;
   row4_sum4(z, jq, rk, dn2);  // bitwise the four row4_sums, 21 instructions instead of 40
-#else
-  z = row4_sum(za);
-  jq = row4_sum(jl);
-  rk = row4_sum(ra);
-  dn2 = row4_sum(s1);
-#endif
   beta = row4_sum(s2);
 }
 
@@ -281,7 +258,7 @@ __device__ __forceinline__ void gi16_add(GIState<16>& S, RegFactors& F, double* 
   if (lane <= q) F.sB[lane * kBS + q] = lane < q ? -rk * ia : ia;
   if (lane < q) F.sB[q * kBS + lane] = 0.0;
   // R_A(w, q) = d_w (w < q), R_A(q, q) = alpha: lanes (i < 4, b) write entry 4b + i
-  if (!MPCT_QP16_BDROP) {
+  {
     const int w = 4 * b + i;
     if (i < 4 && w < q) sRA[w * M + q] = sel4v(d, i);
     if (lane == 0) sRA[q * M + q] = alpha;
@@ -345,61 +322,6 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
   // row kd of B G' leaves (lanes = columns)
   if (lane < q - 1) {
     for (int w = kd; w < q - 1; ++w) sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
-  }
-  const int qn = q - 1;
-  if (i == qn) {
-    S.uw = 0.0;
-    S.ww = -1;
-  }
-  S.q = qn;
-  lds_sync();
-}
-
-// remove active constraint kd with B = R_A^-1 alone (the band kernel's band_drop_b, DESIGN §11
-// round 5): R_A E (column kd removed) is re-triangularised by rotations on rows (jj, jj + 1) that
-// turn B's row kd into a multiple of e_{q-1}; rotation jj zeroes the running entry x of that row
-// against y = B(kd, jj + 1), cs = y / r, sn = -x / r, r = |B(kd, kd..jj+1)|, all from one 16-lane
-// prefix sum.  J's columns take the rotations in registers as before; each lane w < q sweeps its
-// row of B through them with the running entry in a register and writes it one row up below kd
-// (row kd leaves).  No R_A, no LDS round trip or lds_sync per rotation.  B's rows keep explicit
-// zeros left of the diagonal, and the sweep writes those zeros too.
-template <class Mark>
-__device__ __forceinline__ void gi16_drop_b(GIState<16>& S, RegFactors& F, int kd, const Mark& mark) {
-  const int lane = qlane(), i = lane & 15;
-  const int q = S.q;
-  double* sB = F.sB;
-  const int idk = __builtin_amdgcn_readlane(S.ww, kd);
-  mark(S, idk, false);
-  lds_sync();  // B's columns written by the adds
-  {
-    const double un = lane_next<16>(S.uw);
-    const int wn = lane_next_i<16>(S.ww);
-    if (i >= kd && i < q - 1) {
-      S.uw = un;
-      S.ww = wn;
-    }
-  }
-  // rotation jj's parameters on lane jj (every row block computes the same)
-  const double y = (i >= kd && i < q) ? sB[kd * kBS + i] : 0.0;
-  const double s2 = block_prefix<16>(y * y, i, 16, true, nullptr);  // |B(kd, kd..i)|^2
-  const double yn = lane_next<16>(y), r2 = lane_next<16>(s2);
-  double cs = 1.0, sn = 0.0;
-  if (i >= kd && i < q - 1 && r2 > 0.0) {
-    const double x = i == kd ? y : (s2 > 0.0 ? s2 * rsq_nr(s2) : 0.0);
-    const double ri = rsq_nr(r2);
-    cs = yn * ri;
-    sn = -x * ri;
-  }
-  double cb = lane < q ? sB[lane * kBS + kd] : 0.0;
-  const int wdst = lane > kd ? lane - 1 : lane;
-#pragma nounroll
-  for (int jj = kd; jj < q - 1; ++jj) {
-    const double c = bcast(cs, jj), sg = bcast(sn, jj);
-    rb_rotate_cols(F.J, jj, c, sg);
-    const double nb = lane < q ? sB[lane * kBS + jj + 1] : 0.0;
-    if (lane < q && lane != kd) sB[wdst * kBS + jj] = c * cb + sg * nb;
-    cb = -sg * cb + c * nb;
-    S.nrot += 1;
   }
   const int qn = q - 1;
   if (i == qn) {
@@ -512,44 +434,17 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
             la = fma(Bl[r], w[r], la);
           }
         });
-#if MPCT_QP16_SUM4
         row4_sum2(xa, la);
         xm = xu + xa;
         const double lam = la;
-#else
-        xm = xu + row4_sum(xa);
-        const double lam = row4_sum(la);
-#endif
         if (i < q) S.uw = lam;
-#if MPCT_QP16_WARM_DROPALL
-        // every constraint with a negative multiplier leaves before the next solve (highest index
-        // first, so the lower ones keep their lanes); the one-at-a-time form re-solves after each
-        unsigned long long neg = __ballot(i < q && lam < 0.0) & 0xFFFFull;
-        if (neg == 0) break;
-        while (neg) {
-          const int kd = 63 - __builtin_clzll(neg);
-          neg &= ~(1ull << kd);
-          const int qd = S.q;
-#ifdef MPCT_PROFILE
-          pacc[PROF_QROT] += (unsigned long long)(qd - 1 - kd) * kProfCount;
-#endif
-          if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kd, mark);
-          else gi16_drop(S, F, sRA, M, kd, mark);
-          const double cn = lane_next<16>(c);  // c follows the ids
-          if (i >= kd && i < qd - 1) c = cn;
-          else if (i == qd - 1) c = 0.0;
-          ++it;
-        }
-#else
         double lmin = i < q ? lam : INFINITY;
         int kd = i;
         qargmin<16>(lmin, kd, 0);
         if (!(lmin < 0.0)) break;
 #ifdef MPCT_PROFILE
         pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
-#endif
-        if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kd, mark);
-        else gi16_drop(S, F, sRA, M, kd, mark);
+        gi16_drop(S, F, sRA, M, kd, mark);
         {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
           const double cn = lane_next<16>(c);
           if (i >= kd && i < q - 1) c = cn;
@@ -632,8 +527,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
 #ifdef MPCT_PROFILE
       pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kdrop) * kProfCount;
 #endif
-      if (MPCT_QP16_BDROP) gi16_drop_b(S, F, kdrop, mark);
-      else gi16_drop(S, F, sRA, M, kdrop, mark);
+      gi16_drop(S, F, sRA, M, kdrop, mark);
       PSTAMP(PROF_QDROP);
       if (it >= maxit) {
         *st |= MPCT_ST_QP_MAXITER_;

@@ -72,15 +72,6 @@ __device__ __forceinline__ int sm_lane() {
 // LDS, so 16 workgroups fit a CU and the metric's 4096 simulations run in one round.  Against three
 // waves: bitwise the same results, 3.11-3.19 against 3.38-3.46 ms at 8192 candidates, the same
 // 2.21-2.24 ms at 4096 (profiles/r04b_small_ab.txt)
-// MPCT_SM_RL_MOVES=1: u(t-1) of the row's MV and the first moves by readlane + select instead of
-// ds_bpermute.  Bitwise the same; 4,096 candidates 2.011 / 2.033 against 2.042 / 2.052 ms, but 8,192
-// 2.883 against 2.828 ms and the heaviest 256 unchanged (gpurun_out/r05r): not kept
-#ifndef MPCT_SM_RL_MOVES
-#define MPCT_SM_RL_MOVES 0
-#endif
-#ifndef MPCT_SM_EARLY_XS
-#define MPCT_SM_EARLY_XS 1
-#endif
 __global__ void __launch_bounds__(64, 4)
     gpc_small_kernel(const DevScenario sc, long long C, int nref, const int* __restrict__ N2v,
                      const int* __restrict__ Nuv, const double* __restrict__ deltav,
@@ -176,11 +167,9 @@ __global__ void __launch_bounds__(64, 4)
     lds_sync();  // rings of step t - 1 -> this step's plant terms and product
     // ---- plant (exact difference equations of every entry, lsim)
     const double hv = lds[pbase + ((t - pc) & pmask)];
-#if MPCT_SM_EARLY_XS
     // the y update's reads of its own state (step t - 1's nabla y, nabla^2 y), issued with the ring
     // read so that their latency hides under the plant's reductions (every lane reads a valid slot)
     const double o1e = lds[L.xy + yoff + 1], o2e = lds[L.xy + yoff + 2];
-#endif
     const double ye = row4_sum(pcoef * hv);  // y_e(t) on lane e of every row
     double yi = ye + dppd<kQx1>(ye);
     yi += dppd<kQx2>(yi);  // y_i(t) on every lane of quad i
@@ -193,11 +182,7 @@ __global__ void __launch_bounds__(64, 4)
         // nabla^1,2 y(t-1) are the state's own entries of the last step (read before they are
         // overwritten); y(t-1) stays in a register
         double* xs = lds + L.xy + yoff;
-#if MPCT_SM_EARLY_XS
         const double o1 = o1e, o2 = o2e;
-#else
-        const double o1 = xs[1], o2 = xs[2];
-#endif
         const double n1 = yi - yd0, n2 = n1 - o1, n3 = n2 - o2;
         xs[0] = yi - r_t;
         if (nyh > 1) xs[1] = n1;
@@ -244,14 +229,7 @@ __global__ void __launch_bounds__(64, 4)
     PSTAMP(PROF_UNC);
     // ---- QP (gpc_qp16.h): u(t-1) of the row's MV from lane n
     double xq;
-#if MPCT_SM_RL_MOVES
-    // u(t-1) of the row's MV: lanes 0..nu-1 hold it; three readlanes (uniform) and a select instead
-    // of a ds_bpermute round trip on the step's chain (nu <= 3 in this kernel)
-    const double u0 = bcast(uprev, 0), u1 = bcast(uprev, 1), u2 = bcast(uprev, 2);
-    const double up_row = rcn.n == 0 ? u0 : (rcn.n == 1 ? u1 : u2);
-#else
     const double up_row = __shfl(uprev, rcn.n, kWave);
-#endif
     iters += gi_qp16<true>(lds + L.rinv, lds + L.ra, M, Nu, rcn, up_row, xu, tol, maxit, &st, gis, rf,
                      kGiRebuild16, xq
 #ifdef MPCT_PROFILE
@@ -262,12 +240,7 @@ __global__ void __launch_bounds__(64, 4)
     // ---- u update (lane n < nu): first move of MV n, plant input ring, past-control ring
     {
       const int l = sm_lane();
-#if MPCT_SM_RL_MOVES
-      const double d0 = bcast(xq, 0), d1 = bcast(xq, Nu), d2 = bcast(xq, 2 * Nu < 64 ? 2 * Nu : 0);
-      const double du = l == 0 ? d0 : (l == 1 ? d1 : d2);
-#else
       const double du = __shfl(xq, l < nu ? l * Nu : 0, kWave);
-#endif
       if (l < nu) {
         const double un = uprev + du;
         uprev = un;

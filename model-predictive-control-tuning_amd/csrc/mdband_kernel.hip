@@ -25,7 +25,6 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
-#include <type_traits>
 
 #include "gi_core.h"
 #include "launch_fan.h"
@@ -52,52 +51,24 @@
 #define MPCT_BAND_RELTOL 1e-12
 #endif
 constexpr double kRelTol = MPCT_BAND_RELTOL;
-// the output rows' inverse norms |n o D|^-1 (the constraint choice and the termination test): float
-// (4 B per row side) or, MPCT_BAND_RN_F64, double as the oracle computes them
-#ifndef MPCT_BAND_RN_F64
-#define MPCT_BAND_RN_F64 0
-#endif
-typedef std::conditional_t<MPCT_BAND_RN_F64 != 0, double, float> rn_t;
-// every class keeps B = R_A^-1 instead of R_A, in R_A's packed place (band_drop_b): the dual direction r = R_A^-1 d, the warm start's R_A'w = c and lambda = R_A^-1 w
-// become products over the active set instead of serial substitutions (one broadcast per active
-// constraint, q ~ 41 on config 3's slowest simulations), and a drop's rotations come from B's row
-// instead of a chain of LDS round trips through R_A.  MPCT_BAND_EXB=0 keeps R_A in every class
-#ifndef MPCT_BAND_EXB
-#define MPCT_BAND_EXB 1
-#endif
-// the classes that keep B (MAXM, bits: 16 -> 1, 32 -> 2, 64 -> 4).  Config-3 grid: 64 only 0.913 s,
-// 32 and 64 0.897 s, all three 0.894 s (gpurun_out/r05k)
-#ifndef MPCT_BAND_EXB_CLASSES
-#define MPCT_BAND_EXB_CLASSES 7
-#endif
+// the output rows' inverse norms |n o D|^-1 (the constraint choice and the termination test) in
+// float, 4 B per row side: doubles, as the oracle computes them, measured no closer to the C port and
+// slower (grid 1.22 against 0.96 s)
+typedef float rn_t;
+// The QP keeps B = R_A^-1 instead of R_A, in R_A's packed place (band_drop_b): the dual direction
+// r = R_A^-1 d, the warm start's R_A'w = c and lambda = R_A^-1 w become products over the active set
+// instead of serial substitutions (one broadcast per active constraint, q ~ 41 on config 3's
+// slowest simulations), and a drop's rotations come from B's row instead of a chain of LDS round
+// trips through R_A (grid 0.95 -> 0.89 s, slowest simulation 147 -> 117 ms).
+// Measured and not kept there, all bitwise equal: an odd column stride for J, an LDS copy of the
+// QP's step rows, eight taps per trip in the output-row scan
 
 namespace mpct {
-
-// J's column stride.  MPCT_BAND_LDJ_ODD=1 pads it to an odd count, so that dvec's reads (lane k
-// walks column k of JT) fall in distinct LDS banks for 32 lanes (config 3's Mz = 46 and 10 are
-// even).  The kernel's LDS bank conflicts are 4.6 % of its LDS cycles (profiles/r05_sq_workloads.json)
-// and the padding measured 0.912 / 0.913 s against 0.895 / 0.896 s for the grid (gpurun_out/r05o)
-// MPCT_BAND_STEP_LDS=1: the QP's step rows copied to LDS when they fit the simulation's tier
-// (band_layout).  Bitwise the same results; grid 0.922 / 0.923 s against 0.925 / 0.927 s, slowest
-// simulation 116 against 117 ms (gpurun_out/r05p): within noise, so the QP reads L1 / L2
-// MPCT_BAND_YHAT8=1: the scan's prediction takes eight taps per trip.  Bitwise the same; grid
-// 0.908 / 0.910 against 0.895 / 0.897 s, slowest simulation unchanged (gpurun_out/r05r): not kept
-#ifndef MPCT_BAND_YHAT8
-#define MPCT_BAND_YHAT8 0
-#endif
-#ifndef MPCT_BAND_STEP_LDS
-#define MPCT_BAND_STEP_LDS 0
-#endif
-#ifndef MPCT_BAND_LDJ_ODD
-#define MPCT_BAND_LDJ_ODD 0
-#endif
-__host__ __device__ constexpr int band_ldj(int Mz) { return MPCT_BAND_LDJ_ODD ? (Mz | 1) : Mz; }
 
 struct BandLayout {
   int ri, jt, ra, dv, nv, xc, gv, sl, ob, fr, bits, du, uprev, ucum, ye, yeh, uring, tail, sext, rn, plb, pla,
       mzb, mza, total;
   int yh, ur, ts;  // entry output ring, input ring (powers of two) and tail stride of this scenario
-  int stq;         // the QP's copy of the step rows (s_in(0..N2)), or -1 (band_layout)
 };
 
 __host__ __device__ inline int pow2_at_least(int n) {
@@ -126,8 +97,8 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
   L.ri = take(full_ri ? Mz * Mz : Mz);
-  L.jt = take(Mz * band_ldj(Mz));  // J, column-major JT[k*ldj + i] = J(i,k) (R parks here, stride Mz)
-  L.ra = take(ra_packed_size(Mz));  // R_A, packed (gi_core.h RAPacked), or B = R_A^-1 in its place (band_drop_b)
+  L.jt = take(Mz * Mz);  // J, column-major JT[k*Mz + i] = J(i,k)
+  L.ra = take(ra_packed_size(Mz));  // B = R_A^-1, packed as R_A would be (gi_core.h RAPacked)
   L.dv = take(Mz);       // d = J'n
   L.nv = take(Mz);       // staged normal n_p
   L.xc = take(Mz);       // QP iterate
@@ -151,29 +122,12 @@ __host__ __device__ inline BandLayout band_layout(const DevScenario& sc, int N2,
   L.uring = take(ncopy * nin * L.ur);
   L.tail = take(ne * L.ts);  // model entry tails of the window (mz_na - 1 entries each)
   L.sext = take(ne);            // model entry window extensions
-  L.rn = take(my * N2 * (MPCT_BAND_RN_F64 ? 2 : 1));  // output rows' inverse norms: 2 rn_t (upper, lower) per row
+  L.rn = take(my * N2);  // output rows' inverse norms: 2 floats (upper, lower) per row
   L.plb = take(ne * sc.pl_maxbc);  // compact: taps from the first nonzero one
   L.pla = take(ne * sc.pl_maxa);
   L.mzb = take(ne * sc.mz_maxbc);
   L.mza = take(ne * sc.mz_maxa);
   L.total = (o + 1) & ~1;
-  // the step rows s_in(0..N2) the QP reads in every output-row scan (yhat) and normal (dvec), copied
-  // to LDS when they fit under the LDS tier the simulation occupies anyway (the same values: bitwise
-  // the same results); otherwise the QP reads the scenario's table through L1 / L2
-  L.stq = -1;
-  if (MPCT_BAND_STEP_LDS) {
-    const int nq = (my * nu * (N2 + 1) + 1) & ~1;
-    long long cap = 0;
-    for (long long c : kBandCapsKb)
-      if (c * 1024 >= (long long)L.total * 8) {
-        cap = c * 1024;
-        break;
-      }
-    if (cap && (long long)(L.total + nq) * 8 <= cap) {
-      L.stq = L.total;
-      L.total += nq;
-    }
-  }
   return L;
 }
 
@@ -193,8 +147,6 @@ struct BandBAdd {
     if (lane == q && q > 0) bt[bt_idx(q, q - 1)] = 0.0;
     if (lane == q + 1) bt[bt_idx(q + 1, q)] = 0.0;
   }
-  __device__ __forceinline__ void rot(int, int, double, double) const {}
-  __device__ __forceinline__ void drop_rows(int, int) const {}
 };
 // lane w < q: sum_{k < q} B(w,k) c_k, c in LDS
 __device__ __forceinline__ double bt_mul(const double* bt, const double* c, int q) {
@@ -261,7 +213,7 @@ __device__ __forceinline__ double wave_prefix_sum(double v) {
 // The same factorisation as the R_A form up to the signs of R_new's rows (Givens QR is unique up
 // to them), which J and B carry consistently.  cs / sn are staged in sc_ / ss_ (Mz doubles each).
 template <int MAXM, class Mark>
-__device__ __forceinline__ void band_drop_b(GIState<MAXM>& S, double* sJT, double* bt, int Mz, int ldj, int kd,
+__device__ __forceinline__ void band_drop_b(GIState<MAXM>& S, double* sJT, double* bt, int Mz, int kd,
                                             const Mark& mark, double* sc_, double* ss_) {
   const int lane = threadIdx.x;
   const int q = S.q;
@@ -293,20 +245,20 @@ __device__ __forceinline__ void band_drop_b(GIState<MAXM>& S, double* sJT, doubl
   lds_sync();
   // J's columns (lanes = rows of J) and B's rows by slot (lanes = rows w < q)
   const bool jrow = lane < Mz, brow = lane < q;
-  double cj = jrow ? sJT[kd * ldj + lane] : 0.0;
+  double cj = jrow ? sJT[kd * Mz + lane] : 0.0;
   double cb = (brow && lane <= kd + 1) ? bt[bt_idx(lane, kd)] : 0.0;
   const int wdst = lane > kd ? lane - 1 : lane;  // B's row kd leaves: rows below move up one
   for (int jj = kd; jj < q - 1; ++jj) {
     const double cs = sc_[jj], sn = ss_[jj];
-    const double nj = jrow ? sJT[(jj + 1) * ldj + lane] : 0.0;
+    const double nj = jrow ? sJT[(jj + 1) * Mz + lane] : 0.0;
     const double nb = (brow && lane <= jj + 2) ? bt[bt_idx(min(lane, jj + 2), jj + 1)] : 0.0;
-    if (jrow) sJT[jj * ldj + lane] = cs * cj + sn * nj;
+    if (jrow) sJT[jj * Mz + lane] = cs * cj + sn * nj;
     const double vb = cs * cb + sn * nb;
     if (brow && lane != kd && wdst <= jj + 1) bt[bt_idx(wdst, jj)] = vb;
     cj = -sn * cj + cs * nj;
     cb = -sn * cb + cs * nb;
   }
-  if (jrow) sJT[(q - 1) * ldj + lane] = cj;
+  if (jrow) sJT[(q - 1) * Mz + lane] = cj;
   const int qn = q - 1;
   if (lane == qn) {
     S.uw = 0.0;
@@ -391,10 +343,7 @@ __global__ void __launch_bounds__(64, 1)
   const int tls = sc.tlen;
   double* sRi = lds + L.ri;
   double* sJT = lds + L.jt;
-  const int ldj = band_ldj(Mz);
   double* sRA = lds + L.ra;
-  const RAPacked rap{};
-  constexpr bool EXB = MPCT_BAND_EXB != 0 && ((MPCT_BAND_EXB_CLASSES >> (MAXM == 64 ? 2 : MAXM == 32 ? 1 : 0)) & 1);
   double* sBT = lds + L.ra;
   double* sd = lds + L.dv;
   double* snv = lds + L.nv;
@@ -418,9 +367,6 @@ __global__ void __launch_bounds__(64, 1)
   double* smzb = lds + L.mzb;
   double* smza = lds + L.mza;
   const double* __restrict__ sstep = sc.step;  // global, L1/L2-resident
-  const bool stq = L.stq >= 0;                  // the QP's LDS copy of the step rows (band_layout)
-  const double* sstq = stq ? lds + L.stq : sstep;
-  const int tlq = stq ? N2 + 1 : sc.tlen;
 
   // ------------------------------------------------------------------ prologue
   for (int e = lane; e < ne * sc.pl_maxbc; e += kWave) {
@@ -434,11 +380,6 @@ __global__ void __launch_bounds__(64, 1)
   }
   for (int e = lane; e < ne * sc.mz_maxa; e += kWave) smza[e] = sc.mz_a[e];
   for (int e = lane; e < 4 * my; e += kWave) sob[e] = sc.obnd[e];
-  if (stq)
-    for (int e = lane; e < my * nu * (N2 + 1); e += kWave) {
-      const int in = e / (N2 + 1), t = e - in * (N2 + 1);
-      lds[L.stq + e] = sstep[in * sc.tlen + t];
-    }
   for (int e = lane; e < L.plb - L.fr; e += kWave) lds[L.fr + e] = 0.0;
   const bool row = lane < Mz;  // QP-row lanes: moves 0..M-1, eps at M
   RowCons rcn;
@@ -577,11 +518,11 @@ __global__ void __launch_bounds__(64, 1)
   // J = R^-1 (gi_load_rinv), or its diagonal in band mode
   auto load_j = [&]() __attribute__((always_inline)) {
     if (any_q) {
-      gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row, ldj);
+      gi_load_rinv<MAXM>(gis, sJT, sRi, Mz, row);
     } else {
       if (row) {
         const double dj = sRi[lane];
-        for (int k = 0; k < Mz; ++k) sJT[k * ldj + lane] = k == lane ? dj : 0.0;
+        for (int k = 0; k < Mz; ++k) sJT[k * Mz + lane] = k == lane ? dj : 0.0;
       }
       gis.nrot = 0;
       gis.jinit = true;
@@ -594,25 +535,9 @@ __global__ void __launch_bounds__(64, 1)
     double a0 = F[g], a1 = 0.0;
     const int lmax = min(Nu - 1, k + 1);
     for (int n = 0; n < nu; ++n) {
-      const double* sp = sstq + (i * nu + n) * tlq + (k + 1);
+      const double* sp = sstep + (i * nu + n) * tls + (k + 1);
       const double* xp = sxc + n * Nu;
       int l = 0;
-#if MPCT_BAND_YHAT8
-      for (; l + 7 <= lmax; l += 8) {  // eight taps' loads in flight, the same accumulation order
-        const double s0 = sp[-l], s1 = sp[-l - 1], s2 = sp[-l - 2], s3 = sp[-l - 3];
-        const double s4 = sp[-l - 4], s5 = sp[-l - 5], s6 = sp[-l - 6], s7 = sp[-l - 7];
-        const double x0 = xp[l], x1 = xp[l + 1], x2 = xp[l + 2], x3 = xp[l + 3];
-        const double x4 = xp[l + 4], x5 = xp[l + 5], x6 = xp[l + 6], x7 = xp[l + 7];
-        a0 += s0 * x0;
-        a1 += s1 * x1;
-        a0 += s2 * x2;
-        a1 += s3 * x3;
-        a0 += s4 * x4;
-        a1 += s5 * x5;
-        a0 += s6 * x6;
-        a1 += s7 * x7;
-      }
-#endif
       // four taps per trip, their loads issued together; the accumulation order (even taps into
       // a0, odd into a1) is the two-tap loop's
       for (; l + 3 <= lmax; l += 4) {
@@ -656,7 +581,7 @@ __global__ void __launch_bounds__(64, 1)
         const int q = p - base, g = q >> 1, i = g / N2, k = g - i * N2;
         if (lane < M) {
           const int tt = k + 1 - rcn.l;
-          nvv = tt >= 0 ? sstq[(i * nu + rcn.n) * tlq + tt] : 0.0;
+          nvv = tt >= 0 ? sstep[(i * nu + rcn.n) * tls + tt] : 0.0;
           if (!(q & 1)) nvv = -nvv;
         } else {
           nvv = sob[((q & 1) ? 2 : 3) * my + i];
@@ -667,7 +592,7 @@ __global__ void __launch_bounds__(64, 1)
     lds_sync();
     double dk = 0.0;
     if (row) {
-      const double* jc = sJT + lane * ldj;
+      const double* jc = sJT + lane * Mz;
       double d1 = 0.0;
       int r = 0;
       for (; r + 3 < Mz; r += 4) {  // four terms' loads together, the two-term loop's order
@@ -832,13 +757,10 @@ __global__ void __launch_bounds__(64, 1)
           const double dk = dvec(p);
           const double beta = qsum<MAXM>(lane >= v && row ? dk * dk : 0.0);
           lds_sync();
-          const double zm = gi_z(sJT, sd, v, Mz, row, ldj);
+          const double zm = gi_z(sJT, sd, v, Mz, row);
           const double uk = gis.uw;
-          if constexpr (EXB)
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, RANone{},
-                         BandBAdd{sBT, bt_mul(sBT, sd, v)}, ldj);
-          else
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, rap, GINoExt{}, ldj);
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, 0.0, row, mark, RANone{},
+                       BandBAdd{sBT, bt_mul(sBT, sd, v)});
           if (lane == v) gis.uw = uk;
           ++it;
         }
@@ -863,48 +785,30 @@ __global__ void __launch_bounds__(64, 1)
         double wv = 0.0;
         x = row ? xu : 0.0;
         double lam;
-        if constexpr (EXB) {
-          // w = B'c, then x = x_u + J(:,0:q) w and lambda = B w, three products (w staged in sd)
-          if (row) snv[lane] = cc;
-          lds_sync();
-          wv = bt_tmul(sBT, snv, q);
-          if (row) sd[lane] = lane < q ? wv : 0.0;
-          lds_sync();
-          if (row) {
-            double x1 = 0.0;
-            int v = 0;
-            for (; v + 1 < q; v += 2) {
-              x = fma(sJT[v * ldj + lane], sd[v], x);
-              x1 = fma(sJT[(v + 1) * ldj + lane], sd[v + 1], x1);
-            }
-            if (v < q) x = fma(sJT[v * ldj + lane], sd[v], x);
-            x += x1;
+        // w = B'c, then x = x_u + J(:,0:q) w and lambda = B w, three products (w staged in sd)
+        if (row) snv[lane] = cc;
+        lds_sync();
+        wv = bt_tmul(sBT, snv, q);
+        if (row) sd[lane] = lane < q ? wv : 0.0;
+        lds_sync();
+        if (row) {
+          double x1 = 0.0;
+          int v = 0;
+          for (; v + 1 < q; v += 2) {
+            x = fma(sJT[v * Mz + lane], sd[v], x);
+            x1 = fma(sJT[(v + 1) * Mz + lane], sd[v + 1], x1);
           }
-          lam = bt_mul(sBT, sd, q);
-          lds_sync();  // sd / snv are rewritten by the next dvec or pass
-        } else {
-          // R_A'w = c, x = x_u + J(:,0:q) w; step v's R_A and J entries are loaded one step ahead,
-          // off the chain of broadcasts
-          double ra = lane < Mz ? sRA[rap(0, lane)] : 0.0, jv = row ? sJT[lane] : 0.0;
-          for (int v = 0; v < q; ++v) {
-            const int vn = v + 1 < q ? v + 1 : v;
-            const double ran = lane < Mz ? sRA[rap(vn, lane)] : 0.0, jvn = row ? sJT[vn * ldj + lane] : 0.0;
-            const double w = bcast(cc * gis.rdg, v);
-            if (lane == v) wv = w;
-            if (lane > v && lane < q) cc -= ra * w;
-            if (row) x += jv * w;
-            ra = ran;
-            jv = jvn;
-          }
-          lam = gi_backsub<MAXM>(gis, sRA, Mz, wv, rap);
+          if (v < q) x = fma(sJT[v * Mz + lane], sd[v], x);
+          x += x1;
         }
+        lam = bt_mul(sBT, sd, q);
+        lds_sync();  // sd / snv are rewritten by the next dvec or pass
         if (lane < q) gis.uw = lam;
         double lmin = lane < q ? lam : INFINITY;
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
-        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, ldj, kd, mark, snv, sd);
-        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kd, mark, rap, GINoExt{}, ldj);
+        band_drop_b(gis, sJT, sBT, Mz, kd, mark, snv, sd);
         ++it;
       }
       return row ? x : 0.0;
@@ -975,11 +879,9 @@ __global__ void __launch_bounds__(64, 1)
         const double dn2 = qsum<MAXM>(d2);
         const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
         lds_sync();
-        const double zm = gi_z(sJT, sd, gis.q, Mz, row, ldj);
+        const double zm = gi_z(sJT, sd, gis.q, Mz, row);
         PSTAMP(PROF_QD);
-        double rk;
-        if constexpr (EXB) rk = bt_mul(sBT, sd, gis.q);
-        else rk = gi_backsub<MAXM>(gis, sRA, Mz, dk, rap);
+        const double rk = bt_mul(sBT, sd, gis.q);
         double t1 = INFINITY;
         int kdrop = 0x7fffffff;
         if (lane < gis.q && rk > 0.0) {
@@ -1001,15 +903,11 @@ __global__ void __launch_bounds__(64, 1)
         upm += t;
         sp += t * beta;
         if (full) {
-          if constexpr (EXB)
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk}, ldj);
-          else
-            gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, rap, GINoExt{}, ldj);
+          gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk});
           PSTAMP(PROF_QADD);
           break;
         }
-        if constexpr (EXB) band_drop_b(gis, sJT, sBT, Mz, ldj, kdrop, mark, snv, sd);
-        else gi_drop<MAXM>(gis, sJT, sRA, Mz, kdrop, mark, rap, GINoExt{}, ldj);
+        band_drop_b(gis, sJT, sBT, Mz, kdrop, mark, snv, sd);
         PSTAMP(PROF_QDROP);
         if (git >= maxit) {
           st |= MPCT_ST_QP_MAXITER_;

@@ -53,22 +53,16 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // DPP moves.  Controls whose every lane has a source within its row (quad_perm, row_mirror,
 // row_half_mirror, row_newbcast) use v_mov_b32_dpp without an `old` operand: the update_dpp(0, ..)
 // form makes the compiler zero a fresh register before every move (two v_mov_b32 per double,
-// ~60 per Goldfarb-Idnani step of the metric kernel).  The row shifts (row_shl / row_shr: lanes at
-// the row's edge have no source) set bound_ctrl, which writes 0 to those lanes as old = 0 would,
-// without the zeroed register; MPCT_DPP_OLD0=1 restores update_dpp(0, ..) for them
-#ifndef MPCT_BP_BRANCHY
-#define MPCT_BP_BRANCHY 0
-#endif
-#ifndef MPCT_DPP_OLD0
-#define MPCT_DPP_OLD0 0
-#endif
+// ~60 per Goldfarb-Idnani step of the metric kernel; a double's move pair went from 32 to 13 cycles
+// of dependent latency, tools/latency_probe.hip).  The row shifts (row_shl / row_shr: lanes at the
+// row's edge have no source) set bound_ctrl, which writes 0 to those lanes as old = 0 would,
+// without the zeroed register
 template <int CTRL>
 constexpr bool kDppAllLanes = CTRL < 0x100 || CTRL == 0x140 || CTRL == 0x141 || (CTRL >= 0x150 && CTRL <= 0x15F);
 template <int CTRL>
 __device__ __forceinline__ int dpp32(int v) {
   if constexpr (kDppAllLanes<CTRL>) return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-  else if constexpr (MPCT_DPP_OLD0 == 0) return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
-  else return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  else return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
@@ -382,15 +376,9 @@ __device__ __forceinline__ double block_prefix(double x, int l, int Nu, bool row
     // the first three stages run whatever Nu is (l < Nu masks them): their uniform Nu tests were
     // four SALU / VALU instructions and a branch each, more than the stage they skip
     double pre = x, t;
-#if MPCT_BP_BRANCHY
-    if (Nu > 1) { t = dppd<0x111>(pre); if (l >= 1) pre += t; }
-    if (Nu > 2) { t = dppd<0x112>(pre); if (l >= 2) pre += t; }
-    if (Nu > 4) { t = dppd<0x114>(pre); if (l >= 4) pre += t; }
-#else
     t = dppd<0x111>(pre); if (l >= 1) pre += t;
     t = dppd<0x112>(pre); if (l >= 2) pre += t;
     t = dppd<0x114>(pre); if (l >= 4) pre += t;
-#endif
     if (Nu > 8) { t = dppd<0x118>(pre); if (l >= 8) pre += t; }
     return pre;
   } else {
