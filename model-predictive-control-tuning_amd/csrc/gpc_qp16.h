@@ -444,6 +444,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         if (!(lmin < 0.0)) break;
 #ifdef MPCT_PROFILE
         pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
+#endif
         gi16_drop(S, F, sRA, M, kd, mark);
         {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
           const double cn = lane_next<16>(c);
@@ -451,7 +452,6 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
           else if (i == q - 1) c = 0.0;
         }
         ++it;
-#endif
       }
       if (!row) xm = 0.0;
     }
