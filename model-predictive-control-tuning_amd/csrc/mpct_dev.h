@@ -18,6 +18,9 @@ struct WorkOrder {
   bool pending = false;  // `used` has been recorded
 };
 constexpr long long kOrderMinC = 256;  // at most one workgroup per CU: a single round, order is moot
+constexpr int kGramM = 16;                              // QP size of the dispatch-key Gram tables
+constexpr int kGramOut = kGramM * kGramM + kGramM;      // doubles per output and (N2, Nu) block
+constexpr long long kGramMaxBytes = 64ll << 20;         // larger tables are not built
 
 
 constexpr int kMaxOut = 16;    // outputs (my)
@@ -76,6 +79,11 @@ struct DevScenario {
   const int* sm_acol;     // [nx]
   // tables (device pointers into one allocation)
   const double* step;   // [my][nu][tlen]   model step responses s_ij(t), t = 0..tlen-1
+  // dispatch-key Gram tables (work_order.hip order_keys_gpc; nullptr when not built): block
+  // (N2 - 1) numax + Nu - 1, output o at kGramOut o doubles: G_o'G_o (kGramM x kGramM, both
+  // triangles) then G_o'1 (kGramM), G_o = the forced-response matrix of output o (MatG.m); only
+  // for nu Nu <= kGramM and my <= 4
+  const double* gram;
   const double* phi;    // [my*n2max][nx]   free response rows (Diophantine F | deltaUFree Hp)
   const int* n1;        // [my]   first predicted step
   const int* yoff;      // [my]   offset of y_i history (length na_i+1) in the state

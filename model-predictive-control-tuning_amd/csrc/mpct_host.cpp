@@ -859,6 +859,46 @@ static int device_ctx(mpct_scenario* s, int want_dev, DevCtx** out, int occurren
   return MPCT_OK;
 }
 
+// the dispatch key's Gram tables (DevScenario::gram): for every horizon pair (N2, Nu) with
+// nu Nu <= kGramM and every output o, G_o'G_o and G_o'1 of the forced-response matrix
+// G_o(r, n Nu + l) = s_on(n1_o + r - l), r < N2 (MatG.m; zero where the step index is negative).
+// They depend on the scenario alone, so the key forms H = sum_o q_o G_o'G_o + Lambda per candidate
+// from them instead of re-correlating the step table in every workgroup.  Empty when the scenario
+// has no step table, more than 4 outputs, or the tables would exceed kGramMaxBytes
+static void gram_tables(const mpct_scenario* s, std::vector<double>& g) {
+  g.clear();
+  const int my = s->my, nu = s->nu, n2max = s->n2max, numax = s->numax, tlen = s->tlen;
+  if (s->nmpc || s->mdband || my > 4 || nu < 1 || nu > kGramM || s->step.empty()) return;
+  const size_t blk = (size_t)my * kGramOut;
+  if ((long long)((size_t)n2max * numax * blk * 8) > kGramMaxBytes) return;
+  g.assign((size_t)n2max * numax * blk, 0.0);
+  for (int N2 = 1; N2 <= n2max; ++N2)
+    for (int Nu = 1; Nu <= std::min(N2, numax) && nu * Nu <= kGramM; ++Nu) {
+      const int M = nu * Nu;
+      double* b = g.data() + ((size_t)(N2 - 1) * numax + (Nu - 1)) * blk;
+      for (int o = 0; o < my; ++o) {
+        double* go = b + (size_t)o * kGramOut;
+        const int n1 = s->n1[o];
+        const double* so = s->step.data() + (size_t)o * nu * tlen;
+        for (int a = 0; a < M; ++a) {
+          const int na = a / Nu, la = a - na * Nu;
+          const double* sa = so + (size_t)na * tlen + n1 - la;  // sa[r] = s_o,na(n1 + r - la)
+          double cs = 0.0;
+          for (int r = std::max(la - n1, 0); r < N2; ++r) cs += sa[r];
+          go[kGramM * kGramM + a] = cs;
+          for (int bb = a; bb < M; ++bb) {
+            const int nb = bb / Nu, lb = bb - nb * Nu;
+            const double* sb = so + (size_t)nb * tlen + n1 - lb;
+            double h = 0.0;
+            for (int r = std::max(std::max(la, lb) - n1, 0); r < N2; ++r) h += sa[r] * sb[r];
+            go[a * kGramM + bb] = h;
+            go[bb * kGramM + a] = h;
+          }
+        }
+      }
+    }
+}
+
 // a new context on device dev (current): the scenario's tables uploaded, its own stream
 static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   // pack all tables into one allocation, 256-B aligned pieces
@@ -896,6 +936,9 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   size_t o_wsc = put(s->wscale.data(), s->wscale.size() * 8);
   size_t o_xc = put(s->xc.data(), s->xc.size() * 4);
   size_t o_nm = put(s->nm.data(), s->nm.size() * 8);
+  std::vector<double> gram;
+  gram_tables(s, gram);
+  size_t o_gram = put(gram.data(), gram.size() * 8);
   SmallTables smt;
   const bool small = small_plant(s, &smt);
   size_t o_smc = put(smt.coef.data(), smt.coef.size() * 8);
@@ -942,6 +985,7 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   ds.sm_hmask = reinterpret_cast<const int*>(b + o_smm);
   ds.sm_acol = reinterpret_cast<const int*>(b + o_sma);
   ds.step = reinterpret_cast<const double*>(b + o_step);
+  ds.gram = gram.empty() ? nullptr : reinterpret_cast<const double*>(b + o_gram);
   ds.phi = reinterpret_cast<const double*>(b + o_phi);
   ds.n1 = reinterpret_cast<const int*>(b + o_n1);
   ds.yoff = reinterpret_cast<const int*>(b + o_yoff);

@@ -58,9 +58,58 @@ __global__ void order_keys(int kind, long long C, int my, int nu, const int* __r
 // more |z| exceeds the bounds, the more steps run active QP rows.  On the metric grid this
 // estimate ranks the measured QP work with Spearman 0.93 (the weight-ratio key above: 0.58), and
 // dispatching in its order takes 3.44 ms against the weight-ratio key's 3.90 ms and the measured-
-// work order's 3.48 ms (tools/diag/order_key_probe.py).  One wave per candidate: H by lanes
-// over its entries (step-table correlations), Cholesky and the my solves in LDS, lanes over the
-// reference's time steps for the jumps.
+// work order's 3.48 ms (tools/diag/order_key_probe.py).  One wave per candidate, lanes over the
+// reference's time steps for the jumps.  H and the solves by QP size (round 5; the metric's key
+// went 57 -> 45 us with the register Gauss-Jordan and -> 26 us with the Gram tables,
+// profiles/r05_key_stages.txt):
+//   * nu Nu <= 16, my <= 4 (the metric): H = sum_o q_o G_o'G_o + Lambda from the scenario's Gram
+//     tables (mpct_host.cpp gram_tables), then Gauss-Jordan in registers (gj16).  Correlating the
+//     step table in LDS per workgroup took 21 of the 45 us, the LDS Cholesky and solves 21 of 57;
+//   * larger QPs: H by lanes over its entries (step-table correlations in LDS), Cholesky and the
+//     my solves in LDS (the Gauss-Jordan where the tables were too large to build).
+// [H | rhs_0..3] -> [I | H^-1 rhs] by Gauss-Jordan, lane m < M holding row m in registers, the
+// pivot row broadcast by v_readlane (no LDS hand-off per column).  H is SPD, so the pivots need no
+// exchange; false when a pivot is not positive
+__device__ __forceinline__ bool gj16(double (&h)[kGramM], double (&g)[4], int M, int lane) {
+#pragma unroll
+  for (int j = 0; j < kGramM; ++j) {
+    if (j < M) {
+      const double piv = bcast(h[j], j);
+      if (!(piv > 0.0)) return false;
+      const double ip = 1.0 / piv;
+      const bool pr = lane == j;
+      const double f = h[j] * ip;
+#pragma unroll
+      for (int k = j + 1; k < kGramM; ++k) {
+        const double pk = bcast(h[k], j);
+        h[k] = pr ? pk * ip : fma(-f, pk, h[k]);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const double po = bcast(g[o], j);
+        g[o] = pr ? po * ip : fma(-f, po, g[o]);
+      }
+    }
+  }
+  return true;
+}
+
+// this lane's share of sum over (jump j, move m) of |z_jm| / b_n(m), z_j = sum_i d_ji w_i(m), for
+// the nj jump vectors in sD (lanes over (jump, move) pairs; an unbounded MV adds nothing)
+__device__ __forceinline__ double jump_demand(const double* sD, const double* sW, const double* sBn, int nj, int M,
+                                              int my, int nuc, int lane) {
+  double e = 0.0;
+  for (int q = lane; q < nj * M; q += kWave) {
+    const int j = q / M, m = q - j * M, n = m / nuc;
+    const double bn = sBn[n];
+    if (!(bn > 0.0 && bn < INFINITY)) continue;
+    double z = 0.0;
+    for (int i = 0; i < my; ++i) z += sD[j * my + i] * sW[i * M + m];
+    e += fabs(z) / bn;
+  }
+  return e;
+}
+
 __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long long C, int nref,
                                                       const int* __restrict__ N2v, const int* __restrict__ Nuv,
                                                       const double* __restrict__ delta,
@@ -88,7 +137,11 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   double* sBn = sD + kWave * my;     // b_n per MV (read up front, off the jump passes' chain)
   double* sLw = sBn + nu;            // the move weight of each MV (H's diagonal)
   int* sN1 = reinterpret_cast<int*>(sLw + nu);
-  for (int e = lane; e < my * nu * tlen; e += kWave) sS[e] = sc.step[e];
+  // H and the right-hand sides from the scenario's Gram tables (mpct_host.cpp gram_tables) when
+  // they cover this QP size; else correlated here from the step table
+  const bool tab = sc.gram != nullptr && M <= kGramM && my <= 4;
+  if (!tab)
+    for (int e = lane; e < my * nu * tlen; e += kWave) sS[e] = sc.step[e];
   if (lane < my) {
     const double di = fabs(delta[c * my + lane]);
     const double sqi = sc.wsq ? di : sqrt(di);
@@ -102,127 +155,180 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
     sLw[lane] = wl * wl;
   }
   lds_sync();
-  // H(a,b) = sum_i q_i sum_r G_i(r,a) G_i(r,b) + Lambda,  G_i(r, n*Nu + l) = s_in(n1_i + r - l)
-  for (int e = lane; e < M * (M + 1) / 2; e += kWave) {  // lanes over the upper triangle
-    int a = 0, b = e;
-    while (b >= M - a) {
-      b -= M - a;
-      ++a;
-    }
-    b += a;
-    const int na = a / nuc, la = a - na * nuc, nb = b / nuc, lb = b - nb * nuc;
-    const int lm = la > lb ? la : lb;
-    double h = 0.0;
-    for (int i = 0; i < my; ++i) {
-      const int n1 = sN1[i];
-      const double* sa = sS + (i * nu + na) * tlen + n1 - la;  // sa[r] = s_i,na(n1 + r - la)
-      const double* sb = sS + (i * nu + nb) * tlen + n1 - lb;
-      int rr = lm - n1 > 0 ? lm - n1 : 0;  // first row where both step indices are >= 0
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      for (; rr + 3 < n2; rr += 4) {
-        a0 += sa[rr] * sb[rr];
-        a1 += sa[rr + 1] * sb[rr + 1];
-        a2 += sa[rr + 2] * sb[rr + 2];
-        a3 += sa[rr + 3] * sb[rr + 3];
-      }
-      for (; rr < n2; ++rr) a0 += sa[rr] * sb[rr];
-      h += sQ[i] * ((a0 + a1) + (a2 + a3));
-    }
-    if (a == b) h += sLw[na];
-    sH[a * M + b] = h;
-    sH[b * M + a] = h;
-  }
-  // right-hand sides q_i G_i'1 (column sums of G_i); lane (i, m) keeps its entry in a register
-  const bool wl = lane < my * M;
-  const int wi = wl ? lane / M : 0, wm = wl ? lane - wi * M : 0;
-  double w = 0.0;
-  if (wl) {
-    const int n = wm / nuc, l = wm - n * nuc, n1 = sN1[wi];
-    const double* si = sS + (wi * nu + n) * tlen + n1 - l;
-    for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) w += si[rr];
-    w *= sQ[wi];
-  }
-  lds_sync();
-  // Cholesky H = L L': lane i owns row i (column k below the pivot, then its row of the
-  // trailing block; no integer division in the loop)
   bool spd = true;
-  const bool hr = lane < M;
-  for (int k = 0; k < M; ++k) {
-    const double pk = sH[k * M + k];
-    if (!(pk > 0.0)) {
-      spd = false;
-      break;
-    }
-    const double lk = sqrt(pk), il = 1.0 / lk;
-    lds_sync();
-    double lik = 0.0;
-    if (lane == k) sH[k * M + k] = lk;
-    if (hr && lane > k) {
-      lik = sH[lane * M + k] * il;
-      sH[lane * M + k] = lik;
-    }
-    lds_sync();
-    if (hr && lane > k) {  // four columns' loads before their updates (the stores would otherwise
-                           // hold each next load behind them: one LDS round trip per column)
-      int j = k + 1;
-      for (; j + 3 <= lane; j += 4) {
-        const double h0 = sH[lane * M + j], h1 = sH[lane * M + j + 1];
-        const double h2 = sH[lane * M + j + 2], h3 = sH[lane * M + j + 3];
-        const double l0 = sH[j * M + k], l1 = sH[(j + 1) * M + k];
-        const double l2 = sH[(j + 2) * M + k], l3 = sH[(j + 3) * M + k];
-        sH[lane * M + j] = h0 - lik * l0;
-        sH[lane * M + j + 1] = h1 - lik * l1;
-        sH[lane * M + j + 2] = h2 - lik * l2;
-        sH[lane * M + j + 3] = h3 - lik * l3;
+  if (tab) {
+    // lane m < M: row m of H = sum_o q_o G_o'G_o + Lambda and rhs_o(m) = q_o G_o'1(m), straight
+    // from the block of (N2, Nu) (rows are contiguous: 16 doubles per lane and output)
+    const bool hr = lane < M;
+    const int il = hr ? lane : 0;
+    const double* gb = sc.gram + ((size_t)(n2 - 1) * sc.numax + (nuc - 1)) * my * kGramOut;
+    double h[kGramM], g[4];
+#pragma unroll
+    for (int k = 0; k < kGramM; ++k) h[k] = 0.0;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      g[o] = 0.0;
+      if (o < my) {
+        const double q = hr ? sQ[o] : 0.0;
+        const double* go = gb + o * kGramOut;
+#pragma unroll
+        for (int k = 0; k < kGramM; ++k) h[k] = fma(q, go[il * kGramM + k], h[k]);
+        g[o] = q * go[kGramM * kGramM + il];
       }
-      for (; j <= lane; ++j) sH[lane * M + j] -= lik * sH[j * M + k];
+    }
+    const double lw = hr ? sLw[il / nuc] : 0.0;
+#pragma unroll
+    for (int k = 0; k < kGramM; ++k)
+      if (k == lane) h[k] += lw;
+    spd = gj16(h, g, M, lane);
+    if (spd && hr) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+        if (o < my) sW[o * M + lane] = g[o];
     }
     lds_sync();
+  } else {
+    // H(a,b) = sum_i q_i sum_r G_i(r,a) G_i(r,b) + Lambda,  G_i(r, n*Nu + l) = s_in(n1_i + r - l)
+    for (int e = lane; e < M * (M + 1) / 2; e += kWave) {  // lanes over the upper triangle
+      int a = 0, b = e;
+      while (b >= M - a) {
+        b -= M - a;
+        ++a;
+      }
+      b += a;
+      const int na = a / nuc, la = a - na * nuc, nb = b / nuc, lb = b - nb * nuc;
+      const int lm = la > lb ? la : lb;
+      double h = 0.0;
+      for (int i = 0; i < my; ++i) {
+        const int n1 = sN1[i];
+        const double* sa = sS + (i * nu + na) * tlen + n1 - la;  // sa[r] = s_i,na(n1 + r - la)
+        const double* sb = sS + (i * nu + nb) * tlen + n1 - lb;
+        int rr = lm - n1 > 0 ? lm - n1 : 0;  // first row where both step indices are >= 0
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        for (; rr + 3 < n2; rr += 4) {
+          a0 += sa[rr] * sb[rr];
+          a1 += sa[rr + 1] * sb[rr + 1];
+          a2 += sa[rr + 2] * sb[rr + 2];
+          a3 += sa[rr + 3] * sb[rr + 3];
+        }
+        for (; rr < n2; ++rr) a0 += sa[rr] * sb[rr];
+        h += sQ[i] * ((a0 + a1) + (a2 + a3));
+      }
+      if (a == b) h += sLw[na];
+      sH[a * M + b] = h;
+      sH[b * M + a] = h;
+    }
+    // right-hand sides q_i G_i'1 (column sums of G_i); lane (i, m) keeps its entry in a register
+    const bool wl = lane < my * M;
+    const int wi = wl ? lane / M : 0, wm = wl ? lane - wi * M : 0;
+    double w = 0.0;
+    if (wl) {
+      const int n = wm / nuc, l = wm - n * nuc, n1 = sN1[wi];
+      const double* si = sS + (wi * nu + n) * tlen + n1 - l;
+      for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) w += si[rr];
+      w *= sQ[wi];
+    }
+    if (M <= kGramM && my <= 4) {
+      // the Gram tables' size class without its tables (kGramMaxBytes): Gauss-Jordan on the
+      // LDS-built H (a pivot <= 0 marks the candidate heaviest, as the Cholesky's does)
+      if (wl) sW[wi * M + wm] = w;
+      lds_sync();
+      const bool hr = lane < M;
+      double h[kGramM], g[4];
+  #pragma unroll
+      for (int k = 0; k < kGramM; ++k) h[k] = (hr && k < M) ? sH[lane * M + k] : 0.0;
+  #pragma unroll
+      for (int o = 0; o < 4; ++o) g[o] = (hr && o < my) ? sW[o * M + lane] : 0.0;
+      spd = gj16(h, g, M, lane);
+      if (spd && hr) {
+  #pragma unroll
+        for (int o = 0; o < 4; ++o)
+          if (o < my) sW[o * M + lane] = g[o];
+      }
+      lds_sync();
+    } else {
+      lds_sync();
+      // Cholesky H = L L': lane i owns row i (column k below the pivot, then its row of the
+      // trailing block; no integer division in the loop)
+      const bool hr = lane < M;
+      for (int k = 0; k < M; ++k) {
+        const double pk = sH[k * M + k];
+        if (!(pk > 0.0)) {
+          spd = false;
+          break;
+        }
+        const double lk = sqrt(pk), il = 1.0 / lk;
+        lds_sync();
+        double lik = 0.0;
+        if (lane == k) sH[k * M + k] = lk;
+        if (hr && lane > k) {
+          lik = sH[lane * M + k] * il;
+          sH[lane * M + k] = lik;
+        }
+        lds_sync();
+        if (hr && lane > k) {  // four columns' loads before their updates (the stores would otherwise
+                               // hold each next load behind them: one LDS round trip per column)
+          int j = k + 1;
+          for (; j + 3 <= lane; j += 4) {
+            const double h0 = sH[lane * M + j], h1 = sH[lane * M + j + 1];
+            const double h2 = sH[lane * M + j + 2], h3 = sH[lane * M + j + 3];
+            const double l0 = sH[j * M + k], l1 = sH[(j + 1) * M + k];
+            const double l2 = sH[(j + 2) * M + k], l3 = sH[(j + 3) * M + k];
+            sH[lane * M + j] = h0 - lik * l0;
+            sH[lane * M + j + 1] = h1 - lik * l1;
+            sH[lane * M + j + 2] = h2 - lik * l2;
+            sH[lane * M + j + 3] = h3 - lik * l3;
+          }
+          for (; j <= lane; ++j) sH[lane * M + j] -= lik * sH[j * M + k];
+        }
+        lds_sync();
+      }
+      if (spd && my * M > kWave) {  // more right-hand side entries than lanes: one lane per output
+        if (lane < my) {
+          double* wr = sW + lane * M;
+          for (int m = 0; m < M; ++m) {
+            const int n = m / nuc, l = m - n * nuc, n1 = sN1[lane];
+            const double* si = sS + (lane * nu + n) * tlen + n1 - l;
+            double acc = 0.0;
+            for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) acc += si[rr];
+            wr[m] = sQ[lane] * acc;
+          }
+          for (int m = 0; m < M; ++m) {
+            double a = wr[m];
+            for (int j = 0; j < m; ++j) a -= sH[m * M + j] * wr[j];
+            wr[m] = a / sH[m * M + m];
+          }
+          for (int m = M - 1; m >= 0; --m) {
+            double a = wr[m];
+            for (int j = m + 1; j < M; ++j) a -= sH[j * M + m] * wr[j];
+            wr[m] = a / sH[m * M + m];
+          }
+        }
+        lds_sync();
+      } else if (spd) {
+        // w_i = H^-1 rhs_i, lanes over (i, m): forward then backward substitution, the solved entry
+        // of each step handed over in LDS
+        for (int m = 0; m < M; ++m) {
+          if (wl && wm == m) {
+            w /= sH[m * M + m];
+            sW[wi * M + m] = w;
+          }
+          lds_sync();
+          if (wl && wm > m) w -= sH[wm * M + m] * sW[wi * M + m];
+        }
+        for (int m = M - 1; m >= 0; --m) {
+          if (wl && wm == m) {
+            w /= sH[m * M + m];
+            sW[wi * M + m] = w;
+          }
+          lds_sync();
+          if (wl && wm < m) w -= sH[m * M + wm] * sW[wi * M + m];
+        }
+        lds_sync();
+      }
+    }
   }
   double est = INFINITY;  // a factorisation that fails: treat as heaviest
-  if (spd && my * M > kWave) {  // more right-hand side entries than lanes: one lane per output
-    if (lane < my) {
-      double* wr = sW + lane * M;
-      for (int m = 0; m < M; ++m) {
-        const int n = m / nuc, l = m - n * nuc, n1 = sN1[lane];
-        const double* si = sS + (lane * nu + n) * tlen + n1 - l;
-        double acc = 0.0;
-        for (int rr = l - n1 > 0 ? l - n1 : 0; rr < n2; ++rr) acc += si[rr];
-        wr[m] = sQ[lane] * acc;
-      }
-      for (int m = 0; m < M; ++m) {
-        double a = wr[m];
-        for (int j = 0; j < m; ++j) a -= sH[m * M + j] * wr[j];
-        wr[m] = a / sH[m * M + m];
-      }
-      for (int m = M - 1; m >= 0; --m) {
-        double a = wr[m];
-        for (int j = m + 1; j < M; ++j) a -= sH[j * M + m] * wr[j];
-        wr[m] = a / sH[m * M + m];
-      }
-    }
-    lds_sync();
-  } else if (spd) {
-    // w_i = H^-1 rhs_i, lanes over (i, m): forward then backward substitution, the solved entry
-    // of each step handed over in LDS
-    for (int m = 0; m < M; ++m) {
-      if (wl && wm == m) {
-        w /= sH[m * M + m];
-        sW[wi * M + m] = w;
-      }
-      lds_sync();
-      if (wl && wm > m) w -= sH[wm * M + m] * sW[wi * M + m];
-    }
-    for (int m = M - 1; m >= 0; --m) {
-      if (wl && wm == m) {
-        w /= sH[m * M + m];
-        sW[wi * M + m] = w;
-      }
-      lds_sync();
-      if (wl && wm < m) w -= sH[m * M + wm] * sW[wi * M + m];
-    }
-    lds_sync();
-  }
   if (spd) {
     // jumps of every reference signal, 64 time steps per pass: lanes flag their step, the jump
     // vectors of the flagged steps are compacted into LDS (ballot prefix), then lanes over (jump,
@@ -233,37 +339,73 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
       const double* rk = r + (long long)k * my * nit;
       for (int t0 = 1; t0 < nit; t0 += 8 * kWave) {
         // the jump flags of eight passes first: their loads are independent, so they are issued
-        // together (one global-memory round trip per output instead of one per pass)
+        // together (one global-memory round trip per output instead of one per pass).  With my <= 4
+        // the jump vectors stay in registers, and when the eight passes hold at most 64 jumps they
+        // are compacted into LDS at once: one hand-off for the block instead of a global re-read
+        // and two hand-offs per pass with a jump
         unsigned jm = 0;
-        for (int i = 0; i < my; ++i) {
-          const double* ri = rk + i * nit;
+        double dv[8][4];
+        if (my <= 4) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const double* ri = rk + (i < my ? i : 0) * nit;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+              const int t = t0 + p * kWave + lane;
+              const int tc = t < nit ? t : nit - 1;
+              const double a = ri[tc], b = ri[tc - 1];
+              const bool j = i < my && t < nit && a != b;
+              dv[p][i] = j ? a - b : 0.0;
+              if (j) jm |= 1u << p;
+            }
+          }
+        } else {
+          for (int i = 0; i < my; ++i) {
+            const double* ri = rk + i * nit;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+              const int t = t0 + p * kWave + lane;
+              const int tc = t < nit ? t : nit - 1;
+              const double a = ri[tc], b = ri[tc - 1];
+              if (t < nit && a != b) jm |= 1u << p;
+            }
+          }
+        }
+        unsigned long long bal[8];
+        int nj = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          bal[p] = __ballot((jm >> p) & 1u);
+          nj += __popcll(bal[p]);
+        }
+        if (nj == 0) continue;
+        if (my <= 4 && nj <= kWave) {
+          int off = 0;
 #pragma unroll
           for (int p = 0; p < 8; ++p) {
-            const int t = t0 + p * kWave + lane;
-            const int tc = t < nit ? t : nit - 1;
-            const double a = ri[tc], b = ri[tc - 1];
-            if (t < nit && a != b) jm |= 1u << p;
+            if ((jm >> p) & 1u) {
+              const int slot = off + __popcll(bal[p] & ((1ull << lane) - 1ull));
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (i < my) sD[slot * my + i] = dv[p][i];
+            }
+            off += __popcll(bal[p]);
           }
+          lds_sync();
+          e += jump_demand(sD, sW, sBn, nj, M, my, nuc, lane);
+          lds_sync();
+          continue;
         }
         for (int p = 0; p < 8; ++p) {
           const int t = t0 + p * kWave + lane;
           const bool jmp = (jm >> p) & 1u;
-          const unsigned long long bal = __ballot(jmp);
-          if (!bal) continue;
+          if (!bal[p]) continue;
           if (jmp) {
-            const int slot = __popcll(bal & ((1ull << lane) - 1ull));
+            const int slot = __popcll(bal[p] & ((1ull << lane) - 1ull));
             for (int i = 0; i < my; ++i) sD[slot * my + i] = rk[i * nit + t] - rk[i * nit + t - 1];
           }
           lds_sync();
-          const int nj = __popcll(bal);
-          for (int q = lane; q < nj * M; q += kWave) {
-            const int j = q / M, m = q - j * M, n = m / nuc;
-            const double bn = sBn[n];
-            if (!(bn > 0.0 && bn < INFINITY)) continue;
-            double z = 0.0;
-            for (int i = 0; i < my; ++i) z += sD[j * my + i] * sW[i * M + m];
-            e += fabs(z) / bn;
-          }
+          e += jump_demand(sD, sW, sBn, __popcll(bal[p]), M, my, nuc, lane);
           lds_sync();
         }
       }
