@@ -11,7 +11,7 @@ namespace mpct {
 struct WorkOrder {
   void* buf = nullptr;
   size_t bytes = 0;
-  int* inv = nullptr;       // candidate -> slot (inverse of the last permutation), inside buf
+  const int* perm = nullptr;  // slot -> candidate (the last permutation), inside buf
   void* stage = nullptr;    // staging rows of the ordered launch's cost records (DevResult::stage)
   size_t stage_bytes = 0;
   hipEvent_t used = nullptr;

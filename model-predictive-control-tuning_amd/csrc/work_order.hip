@@ -419,11 +419,6 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   }
 }
 
-__global__ void invert_perm(const int* __restrict__ perm, long long C, int* __restrict__ inv) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < C) inv[perm[i]] = (int)i;
-}
-
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
                      const DevScenario* sc, int nref, const double* r) {
@@ -485,14 +480,7 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
     *err = "hipcub::DeviceRadixSort::SortPairs failed";
     return -3;
   }
-  // the inverse permutation (candidate -> slot) into the free key buffer, for unpermute_results
-  int* inv = reinterpret_cast<int*>(kin);
-  hipLaunchKernelGGL(invert_perm, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, iout, C, inv);
-  if (hipGetLastError() != hipSuccess) {
-    *err = "invert_perm launch failed";
-    return -3;
-  }
-  wo.inv = inv;
+  wo.perm = iout;
   *perm = iout;
   return 0;
 }
@@ -513,14 +501,16 @@ int order_stage(WorkOrder& wo, long long S, int width, double** stage, std::stri
   return 0;
 }
 
-// thread s = c*nref + k of the caller's order reads the staging row of slot inv[c]*nref + k
-__global__ void unpermute_kernel(const double* __restrict__ stage, const int* __restrict__ inv, long long C,
+// thread = staging slot (dispatch order): its row goes to the caller's index perm[c]*nref + k.  A
+// scatter, so the sort's permutation serves as is (no inverse-permutation launch); the reads are
+// coalesced, the few scattered writes (4096 records at the metric) cost the same
+__global__ void unpermute_kernel(const double* __restrict__ stage, const int* __restrict__ perm, long long C,
                                  int nref, int my, int nu, StageRow R, DevResult out) {
-  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long S = C * nref;
-  if (s >= S) return;
-  const long long c = s / nref;
-  const long long slot = (long long)inv[c] * nref + (s - c * nref);
+  if (slot >= S) return;
+  const long long cs = slot / nref;
+  const long long s = (long long)perm[cs] * nref + (slot - cs * nref);
   const double* row = stage + xcd_row(slot, S) * R.w;
   for (int i = 0; i < my; ++i) {
     if (R.j1 >= 0) out.J1[s * my + i] = row[R.j1 + i];
@@ -585,7 +575,7 @@ int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu
                       const DevResult& out, hipStream_t stream, std::string* err) {
   const long long S = C * nref;
   hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream,
-                     static_cast<const double*>(wo.stage), wo.inv, C, nref, my, nu, R, out);
+                     static_cast<const double*>(wo.stage), wo.perm, C, nref, my, nu, R, out);
   if (hipGetLastError() != hipSuccess) {
     *err = "unpermute_results launch failed";
     return -3;
