@@ -419,6 +419,33 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
   }
 }
 
+// ---- rank by counting, for batches up to kCountRankMaxC: the stable ascending position of element
+// i is the number of elements j with (key_j, j) < (key_i, i), so perm[position] = i is exactly the
+// permutation of the stable radix sort.  One wave per two elements, lanes = (element e, chunk h of
+// 32): a lane compares its element against one thirty-second of the keys (128 at the metric's 4096
+// candidates, eight loads in flight), five xor shuffles add the chunks.  One launch instead of the
+// radix sort's three (profiles/r05_key_stages.txt)
+constexpr long long kCountRankMaxC = 8192;
+template <class K>
+__global__ void __launch_bounds__(64) count_rank(const K* __restrict__ keys, int n, int* __restrict__ perm) {
+  const int lane = threadIdx.x;
+  const int e = lane & 1, h = lane >> 1;
+  const int i = blockIdx.x * 2 + e;
+  const bool valid = i < n;
+  const K ki = keys[valid ? i : 0];
+  const int chunk = (n + 31) >> 5;
+  const int j0 = h * chunk, j1 = j0 + chunk < n ? j0 + chunk : n;
+  int cnt = 0;
+#pragma unroll 8
+  for (int j = j0; j < j1; ++j) {
+    const K kj = keys[j];
+    cnt += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+  }
+#pragma unroll
+  for (int m = 2; m < kWave; m <<= 1) cnt += __shfl_xor(cnt, m, kWave);
+  if (valid && h == 0) perm[cnt] = i;
+}
+
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
                      const DevScenario* sc, int nref, const double* r) {
@@ -475,8 +502,15 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
     *err = std::string("dispatch-order key launch failed: ") + hipGetErrorString(ke);
     return -3;
   }
-  if (hipcub::DeviceRadixSort::SortPairs(b + 4 * arr, temp, kin, kout, iin, iout, (int)C, 0, 32, stream) !=
-      hipSuccess) {
+  if (C <= kCountRankMaxC) {
+    hipLaunchKernelGGL(count_rank<unsigned>, dim3((unsigned)((C + 1) / 2)), dim3(kWave), 0, stream,
+                       (const unsigned*)kin, (int)C, iout);
+    if (hipGetLastError() != hipSuccess) {
+      *err = "dispatch-order rank launch failed";
+      return -3;
+    }
+  } else if (hipcub::DeviceRadixSort::SortPairs(b + 4 * arr, temp, kin, kout, iin, iout, (int)C, 0, 32, stream) !=
+             hipSuccess) {
     *err = "hipcub::DeviceRadixSort::SortPairs failed";
     return -3;
   }
@@ -586,17 +620,21 @@ int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu
 // ---- ranking (mpct_rank_device): s_c = sum_j costs[c][j] w[j] in a fixed order, NaN -> +inf,
 // -0 -> +0, mapped to an order-preserving unsigned 64-bit key; the radix sort is stable, so equal
 // costs keep the candidate order
-__global__ void rank_keys(const double* __restrict__ costs, long long C, int k, const double* __restrict__ w,
-                          unsigned long long* __restrict__ key, int* __restrict__ idx) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__device__ __forceinline__ unsigned long long rank_key(const double* __restrict__ costs, long long c, int k,
+                                                       const double* __restrict__ w) {
   double s = 0.0;
   for (int j = 0; j < k; ++j) s = fma(costs[c * k + j], w[j], s);
   if (isnan(s)) s = INFINITY;
   s += 0.0;  // -0 -> +0 (round to nearest)
-  unsigned long long u = (unsigned long long)__double_as_longlong(s);
-  u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-  key[c] = u;
+  const unsigned long long u = (unsigned long long)__double_as_longlong(s);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ void rank_keys(const double* __restrict__ costs, long long C, int k, const double* __restrict__ w,
+                          unsigned long long* __restrict__ key, int* __restrict__ idx) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  key[c] = rank_key(costs, c, k, w);
   idx[c] = (int)c;
 }
 
@@ -610,21 +648,29 @@ int rank_device(const double* costs, long long C, int k, const double* w, int* p
     *err = "hipcub::DeviceRadixSort::SortPairs (size query) failed";
     return -3;
   }
+  const bool counting = C <= kCountRankMaxC;  // keys, then the counting rank (no sort buffers)
   const size_t arr8 = ((size_t)C * 8 + 255) & ~(size_t)255, arr4 = ((size_t)C * 4 + 255) & ~(size_t)255;
   void* buf = nullptr;
-  if (hipMallocAsync(&buf, 2 * arr8 + arr4 + temp, stream) != hipSuccess) {
+  if (hipMallocAsync(&buf, counting ? arr8 + arr4 : 2 * arr8 + arr4 + temp, stream) != hipSuccess) {
     *err = "hipMallocAsync failed (ranking buffers)";
     return -2;
   }
   char* b = static_cast<char*>(buf);
   unsigned long long* kin = reinterpret_cast<unsigned long long*>(b);
   unsigned long long* kout = reinterpret_cast<unsigned long long*>(b + arr8);
-  int* iin = reinterpret_cast<int*>(b + 2 * arr8);
+  int* iin = reinterpret_cast<int*>(b + (counting ? arr8 : 2 * arr8));
   hipLaunchKernelGGL(rank_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, costs, C, k, w, kin, iin);
   int rc = 0;
   if (hipGetLastError() != hipSuccess) {
     *err = "ranking key launch failed";
     rc = -3;
+  } else if (counting) {
+    hipLaunchKernelGGL(count_rank<unsigned long long>, dim3((unsigned)((C + 1) / 2)), dim3(kWave), 0, stream,
+                       (const unsigned long long*)kin, (int)C, perm);
+    if (hipGetLastError() != hipSuccess) {
+      *err = "ranking launch failed";
+      rc = -3;
+    }
   } else if (hipcub::DeviceRadixSort::SortPairs(b + 2 * arr8 + arr4, temp, kin, kout, iin, perm, (int)C, 0, 64,
                                                 stream) != hipSuccess) {
     *err = "hipcub::DeviceRadixSort::SortPairs failed (ranking)";

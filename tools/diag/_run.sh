@@ -1,12 +1,16 @@
 #!/bin/bash
-# scatter unpermute (no invert_perm launch) vs the same without result staging: parity + step time
+# counting rank (order key sort + ranking): GPU suite, metric timing, bench, kernel list
 export TMPDIR=/tmp
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05w"; mkdir -p "$O"
-C="$R/model-predictive-control-tuning_amd/csrc"
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py tests/test_c_abi.py -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 1; }
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05y2"; mkdir -p "$O"
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
-for rep in 1 2; do
-  for L in libmpct.so libmpct_nostage.so; do
-    MPCT_LIB=$C/$L timeout -k 10 120 python3 tools/qab.py 4096 8192 2>&1 | grep kernel || exit 1
-  done
-done
+timeout -k 10 200 python3 tools/qab.py 4096 4096 h256 > "$O/qab.txt" 2>&1 || exit 1; cat "$O/qab.txt"
+for k in 1 2; do timeout -k 10 200 python3 bench.py --no-cpu-baseline > "$O/bench$k.json" 2> "$O/bench$k.err" || exit 1; cut -c1-330 "$O/bench$k.json"; done
+cd /tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$O/kt.log" 2>&1 || exit 1
+python3 - "$O/kt" <<'PY'
+import csv, glob, sys
+for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print(r["Name"][:40], r["Calls"], r["AverageNs"])
+PY
