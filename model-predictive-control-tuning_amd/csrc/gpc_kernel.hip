@@ -622,21 +622,27 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     *err = "nu*nu_max > 64";
     return -4;
   }
+  // ordered launches stage their cost records XCD-major and gather them into the caller's order
+  // afterwards (DevResult::stage): full-line writes instead of 24-B pieces from every L2.  The
+  // staging rows are laid out before the dispatch-order key, whose launch prefills them
   const int* perm = nullptr;
+  DevResult lo = out;
+  bool prefilled = false;
   if (wo) {
-    const int rc =
-        order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err, &sc, nref, r);
+    if (C >= kOrderMinC) {
+      lo.srow = stage_row(out, sc.my, sc.nu);
+      const int rs = lo.srow.w ? order_stage(*wo, C * nref, lo.srow.w, &lo.stage, err) : 0;
+      if (rs) return rs;
+    }
+    const int rc = order_candidates(kOrderGpc, sc.my, sc.nu, C, N2, Nu, delta, lambda, *wo, &perm, stream, err,
+                                    &sc, nref, r, &lo, &prefilled);
     if (rc) return rc;
   }
-  // ordered launches stage their cost records XCD-major and gather them into the caller's order
-  // afterwards (DevResult::stage): full-line writes instead of 24-B pieces from every L2
-  DevResult lo = out;
-  if (perm) {
-    lo.srow = stage_row(out, sc.my, sc.nu);
-    const int rs = lo.srow.w ? order_stage(*wo, C * nref, lo.srow.w, &lo.stage, err) : 0;
-    if (rs) return rs;
+  if (!perm) {
+    lo = out;
+    prefilled = false;
   }
-  int rc = prefill_results(lo, C * nref, sc.my, sc.nu, stream, err);
+  int rc = prefilled ? 0 : prefill_results(lo, C * nref, sc.my, sc.nu, stream, err);
   if (rc) return rc;
   FanScope fs(top_class(maxM) > 16 ? fan : nullptr, stream);
   int k = 0, mlo = 0;

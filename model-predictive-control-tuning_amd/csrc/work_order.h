@@ -28,7 +28,8 @@ constexpr double kOrderEstMaxCost = 1 << 20;
 // candidate's unconstrained move demand (order_keys_gpc); without them, on the weight ratio.
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
-                     const DevScenario* sc = nullptr, int nref = 0, const double* r = nullptr);
+                     const DevScenario* sc = nullptr, int nref = 0, const double* r = nullptr,
+                     const DevResult* pre = nullptr, bool* prefilled = nullptr);
 
 // ascending weighted-cost order of C candidates (mpct_rank_device): device pointers, on `stream`
 int rank_device(const double* costs, long long C, int k, const double* w, int* perm, hipStream_t stream,

@@ -9,6 +9,35 @@
 
 namespace mpct {
 
+// NaN costs, status MPCT_ST_NOT_RUN, 0 iterations for simulation slot s (see prefill_kernel)
+__device__ __forceinline__ void prefill_slot(const DevResult& out, long long s, long long S, int my, int nu) {
+  const double nan = __longlong_as_double(0x7ff8000000000000ll);
+  if (out.stage) {
+    const StageRow& R = out.srow;
+    double* row = out.stage + xcd_row(s, S) * R.w;
+    for (int i = 0; i < my; ++i) {
+      if (R.j1 >= 0) row[R.j1 + i] = nan;
+      if (R.j21 >= 0) row[R.j21 + i] = nan;
+      if (R.j22 >= 0) row[R.j22 + i] = nan;
+    }
+    if (R.jnu >= 0)
+      for (int i = 0; i < nu; ++i) row[R.jnu + i] = nan;
+    if (R.st >= 0) row[R.st] = (double)MPCT_ST_NOT_RUN_;
+    if (R.it >= 0) row[R.it] = 0.0;
+    return;
+  }
+  for (int i = 0; i < my; ++i) {
+    if (out.J1) out.J1[s * my + i] = nan;
+    if (out.j21) out.j21[s * my + i] = nan;
+    if (out.j22) out.j22[s * my + i] = nan;
+  }
+  if (out.Jnu)
+    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = nan;
+  if (out.status) out.status[s] = MPCT_ST_NOT_RUN_;
+  if (out.qp_iters) out.qp_iters[s] = 0;
+}
+
+
 // ---- dispatch order (longest-processing-time first).  The workgroups of a launch start in slot
 // order and a batch larger than the resident slots (4096 simulations, 12 slots per CU at the
 // metric) runs a second, partial round, so a long simulation that starts late sets the kernel
@@ -115,12 +144,16 @@ __global__ void __launch_bounds__(64) order_keys_gpc(const DevScenario sc, long 
                                                       const double* __restrict__ delta,
                                                       const double* __restrict__ lambda,
                                                       const double* __restrict__ r, unsigned* __restrict__ key,
-                                                      int* __restrict__ idx) {
+                                                      int* __restrict__ idx, const DevResult pre, int do_pre) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const long long c = blockIdx.x;
   if (c >= C) return;
   const int lane = threadIdx.x;
   const int my = sc.my, nu = sc.nu, tlen = sc.tlen, nit = sc.nit;
+  // the ordered launch's result prefill (prefill_kernel's records) rides on this launch: candidate
+  // c's wave writes slots c nref .. c nref + nref - 1, so the C waves cover every slot once
+  if (do_pre)
+    for (int k = lane; k < nref; k += kWave) prefill_slot(pre, c * nref + k, C * nref, my, nu);
   const int n2 = N2v[c], nuc = Nuv[c];
   if (lane == 0) idx[c] = (int)c;
   if (!(n2 > 0 && n2 <= sc.n2max && nuc >= 1 && nuc <= sc.numax && nuc <= n2)) {
@@ -448,8 +481,9 @@ __global__ void __launch_bounds__(64) count_rank(const K* __restrict__ keys, int
 
 int order_candidates(int kind, int my, int nu, long long C, const int* N2, const int* Nu, const double* delta,
                      const double* lambda, WorkOrder& wo, const int** perm, hipStream_t stream, std::string* err,
-                     const DevScenario* sc, int nref, const double* r) {
+                     const DevScenario* sc, int nref, const double* r, const DevResult* pre, bool* prefilled) {
   *perm = nullptr;
+  if (prefilled) *prefilled = false;
   if (C < kOrderMinC) return 0;  // one round of workgroups: the order cannot matter
   if (wo.pending && hipStreamWaitEvent(stream, wo.used, 0) != hipSuccess) {
     *err = "hipStreamWaitEvent failed (dispatch-order buffers)";
@@ -492,7 +526,8 @@ int order_candidates(int kind, int my, int nu, long long C, const int* N2, const
   if (kind == kOrderGpc && sc && r && !sc->mdband && !sc->nmpc && Mp <= 64 &&
       hcost <= kOrderEstMaxCost && lds <= 64 * 1024) {
     hipLaunchKernelGGL(order_keys_gpc, dim3((unsigned)C), dim3(kWave), lds, stream, *sc, C, nref, N2, Nu, delta,
-                       lambda, r, kin, iin);
+                       lambda, r, kin, iin, pre ? *pre : DevResult{}, pre ? 1 : 0);
+    if (prefilled) *prefilled = pre != nullptr;
   } else {
     hipLaunchKernelGGL(order_keys, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, kind, C, my, nu, N2,
                        Nu, delta, lambda, kin, iin);
@@ -564,30 +599,7 @@ __global__ void unpermute_kernel(const double* __restrict__ stage, const int* __
 __global__ void prefill_kernel(DevResult out, long long S, int my, int nu) {
   const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
-  const double nan = __longlong_as_double(0x7ff8000000000000ll);
-  if (out.stage) {
-    const StageRow& R = out.srow;
-    double* row = out.stage + xcd_row(s, S) * R.w;
-    for (int i = 0; i < my; ++i) {
-      if (R.j1 >= 0) row[R.j1 + i] = nan;
-      if (R.j21 >= 0) row[R.j21 + i] = nan;
-      if (R.j22 >= 0) row[R.j22 + i] = nan;
-    }
-    if (R.jnu >= 0)
-      for (int i = 0; i < nu; ++i) row[R.jnu + i] = nan;
-    if (R.st >= 0) row[R.st] = (double)MPCT_ST_NOT_RUN_;
-    if (R.it >= 0) row[R.it] = 0.0;
-    return;
-  }
-  for (int i = 0; i < my; ++i) {
-    if (out.J1) out.J1[s * my + i] = nan;
-    if (out.j21) out.j21[s * my + i] = nan;
-    if (out.j22) out.j22[s * my + i] = nan;
-  }
-  if (out.Jnu)
-    for (int i = 0; i < nu; ++i) out.Jnu[s * nu + i] = nan;
-  if (out.status) out.status[s] = MPCT_ST_NOT_RUN_;
-  if (out.qp_iters) out.qp_iters[s] = 0;
+  prefill_slot(out, s, S, my, nu);
 }
 
 bool diag_drop_launch(int k) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # counting rank (order key sort + ranking): GPU suite, metric timing, bench, kernel list
 export TMPDIR=/tmp
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05y2"; mkdir -p "$O"
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05y3"; mkdir -p "$O"
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
 timeout -k 10 200 python3 tools/qab.py 4096 4096 h256 > "$O/qab.txt" 2>&1 || exit 1; cat "$O/qab.txt"
