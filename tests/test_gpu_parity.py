@@ -235,6 +235,15 @@ def test_rank_device_matches_stable_sort(built):
     # the C = prefix form used by the padded multi-rank batch
     got2 = rank_candidates(torch.from_numpy(costs).to(dev), torch.from_numpy(w).to(dev), C=3000).cpu().numpy()
     assert np.array_equal(got2, np.argsort(s[:3000], kind="stable"))
+    # both sides of the counting rank's batch limit (work_order.hip kCountRankMaxC = 8192: counting
+    # rank up to it, hipCUB's radix sort above), odd sizes and one-element batches
+    big = np.concatenate([costs, costs, rng.integers(0, 40, size=(6500, 3)).astype(float)])
+    sb = big @ w
+    sb[np.isnan(sb)] = np.inf
+    tb = torch.from_numpy(big).to(dev)
+    for n in (1, 2, 257, 8191, 8192, 8193, 16500):
+        got = rank_candidates(tb, torch.from_numpy(w).to(dev), C=n).cpu().numpy()
+        assert np.array_equal(got, np.argsort(sb[:n], kind="stable")), n
 
 
 def test_status_edges(env):
