@@ -8,7 +8,8 @@ K=${K:-gpc_kernel.hip}
 OBJS=""
 for u in gpc_kernel gpc_small mdband_kernel nmpc_kernel work_order; do
   if [ "$u.hip" = "$K" ] || { [ "$K" = all ] && [ $u != work_order ]; }; then
-    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c $C/$u.hip -o /tmp/${u}_$NAME.o
+    UF=""; [ $u = gpc_small ] && UF="-mllvm -amdgpu-sched-strategy=max-ilp -mllvm -misched-prera-direction=topdown"  # __graft_entry__.UNIT_FLAGS
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $UF "$@" -c $C/$u.hip -o /tmp/${u}_$NAME.o
     OBJS="$OBJS /tmp/${u}_$NAME.o"
   else
     OBJS="$OBJS $C/$u.o"
