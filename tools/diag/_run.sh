@@ -1,15 +1,15 @@
 #!/bin/bash
-# gpc_small_kernel scheduling on top of max-ilp: pre-RA top-down, post-RA bottom-up (interleaved, bitwise J1 check)
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05i2"; mkdir -p "$O"; C="$R/model-predictive-control-tuning_amd/csrc"
-for rep in 1 2 3; do
-  for L in libmpct.so libmpct_td.so libmpct_pbu.so; do
-    MPCT_LIB=$C/$L QAB_DUMP=$O/${L%.so}.npz timeout -k 10 120 python3 tools/qab.py 4096 h256 2>&1 | grep kernel || exit 1
-  done
+# GPU suite on the max-ILP / top-down metric build, then scheduler variants of the other kernel units
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; O="$R/gpurun_out/r05j2"; mkdir -p "$O"; C="$R/model-predictive-control-tuning_amd/csrc"
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 1; }
+tail -1 "$O/pytest.log"
+timeout -k 10 200 python3 bench.py --no-cpu-baseline > "$O/bench.json" 2> "$O/bench.err" || exit 1; cut -c1-260 "$O/bench.json"
+run() {  # W L rep
+  MPCT_LIB=$C/$2 timeout -k 10 200 python3 bench.py --workload $1 --no-cpu-baseline > "$O/$1.$2.$3.json" 2> "$O/$1.$2.$3.err" || { tail -5 "$O/$1.$2.$3.err"; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], round(d['value']), round(d['ms_per_step'],3), d.get('top_candidate'))" "$O/$1.$2.$3.json" $1 $2
+}
+for rep in 1 2; do
+  for L in libmpct.so libmpct_mtd.so libmpct_mmc.so libmpct_mii.so; do run shell7x5 $L $rep; done
+  for L in libmpct.so libmpct_gtd.so; do run dtc-mc $L $rep; done
+  for L in libmpct.so libmpct_ntd.so; do run vandevusse $L $rep; done
 done
-python3 - "$O" <<'PY'
-import numpy as np, sys
-a = np.load(sys.argv[1] + "/libmpct.npz")
-for v in ("libmpct_td", "libmpct_pbu"):
-    b = np.load(sys.argv[1] + "/%s.npz" % v)
-    print(v, "J1 bitwise equal:", np.array_equal(a["J1"], b["J1"]), "iters equal:", np.array_equal(a["it"], b["it"]))
-PY
