@@ -205,6 +205,33 @@ def pmc_traffic(C, n2, nu):
             pj.get("fp64_counter"))
 
 
+def pmc_workload(workload, kms):
+    """roofline.traffic and fp64_counter_tflops of the other §8d lines from the committed PMC pass over
+    bench.py itself (profiles/pmc_workloads_latest.json, tools/pmc_workloads.sh: per-evaluation HBM bytes
+    and FP64 instruction counts of the workload's kernel family) -- accepted only when that pass
+    profiled this very library (same sha256); the counter rate is its flops over this run's kernel_ms.
+    Returns (bytes per evaluation | None, source note, counter TFLOP/s | None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_workloads_latest.json")
+    if not os.path.exists(p):
+        return None, "no workload PMC pass committed", None
+    try:
+        with open(p) as f:
+            pj = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable profiles/pmc_workloads_latest.json", None
+    mine = lib_sha256()
+    src = "profiles/%s_pmc_workloads.json" % pj.get("tag", "?")
+    if pj.get("lib_sha256") != mine:
+        return None, "%s profiled libmpct.so sha256 %s, this run loaded %s: not used" % (
+            src, str(pj.get("lib_sha256"))[:16], mine[:16]), None
+    e = pj.get(workload) or {}
+    fl = e.get("fp64_flops_per_evaluation")
+    return (e.get("hbm_bytes_per_evaluation"),
+            "%s (PMC pass of bench.py --workload %s on this libmpct.so, sha256 %s; bytes per evaluation)" % (
+                src, workload, mine[:16]),
+            fl / (kms * 1e-3) / 1e12 if fl else None)
+
+
 def latency_roofline():
     """roofline.latency_frac from the committed latency model (profiles/latency_latest.json, written by
     tools/latency_model.py): the dependent chain of the heaviest 256 simulations priced with the
@@ -556,8 +583,12 @@ def other_workload(args):
 
         kname, ibound = kernel_instance(sc), "QP iterations"
     achieved = fl / (kms * 1e-3) / 1e12
+    # the PMC pass profiled one rank's whole grid: only a one-rank run evaluates the same launches
+    traffic, traffic_source, fp64c = pmc_workload(args.workload, kms) if world == 1 else (
+        None, "PMC pass profiled the one-GPU grid", None)
     roof = {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kname, "kernel_ms": kms,
+            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_source,
+            "fp64_counter_tflops": fp64c, "kernel": kname, "kernel_ms": kms,
             "algorithmic_gflop_per_launch": fl / 1e9,
             "iterations_per_sim": float(iters[live].mean()) if live.any() else 0.0,
             "bound_note": "FP64 vector ALU + per-step latency; flops from the DESIGN §7 model with the "

@@ -87,3 +87,25 @@ def test_bench_latency_frac_keyed_to_library(tmp_path, monkeypatch):
     lat.write_text(json.dumps({"lib_sha256": "a" * 64, "latency_frac": 0.3}))
     frac, note = bench.latency_roofline()
     assert frac == 0.3
+
+
+def test_bench_workload_pmc_keyed_to_library(tmp_path, monkeypatch):
+    """the other §8d lines' traffic / counter rate come from the PMC pass over bench.py
+    (tools/pmc_workloads.sh) only when it profiled the loaded library"""
+    import bench
+
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "a" * 64)
+    tr, note, fc = bench.pmc_workload("shell7x5", 900.0)
+    assert tr is None and fc is None and "no workload PMC" in note
+    (tmp_path / "profiles").mkdir()
+    p = tmp_path / "profiles" / "pmc_workloads_latest.json"
+    rec = {"tag": "r99", "shell7x5": {"hbm_bytes_per_evaluation": 6.0e8, "fp64_flops_per_evaluation": 4.5e12}}
+    p.write_text(json.dumps(dict(rec, lib_sha256="b" * 64)))
+    tr, note, fc = bench.pmc_workload("shell7x5", 900.0)
+    assert tr is None and fc is None and "not used" in note
+    p.write_text(json.dumps(dict(rec, lib_sha256="a" * 64)))
+    tr, note, fc = bench.pmc_workload("shell7x5", 900.0)
+    assert tr == 6.0e8 and abs(fc - 5.0) < 1e-12 and "r99_pmc_workloads" in note
+    tr, note, fc = bench.pmc_workload("vandevusse", 190.0)
+    assert tr is None and fc is None
