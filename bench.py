@@ -461,7 +461,8 @@ def main():
 def other_workload(args):
     """SURVEY §8d configs 3-5 through the same harness (barrier + synchronize around K timed steps,
     max over ranks, one JSON line on rank 0).  config 3 (shell7x5): the fixed 65,536-candidate
-    grid of mpct.scenarios.config3_grid split over the ranks (strided) (strong scaling, SURVEY: "65 536-candidate
+    grid of mpct.scenarios.config3_grid split over the ranks by whole cells (mpct.dist.plan_cells_lpt)
+    (strong scaling, SURVEY: "65 536-candidate
     grid sharded over 8xMI355X via RCCL"); config 5 (vandevusse): 4096 NMPC candidates per GPU;
     config 4 (dtc-mc): 10,000 candidates x 32 plant-mismatch draws split over the ranks.  One
     all-gather of the per-candidate cost records, identical ranking on every rank."""
@@ -512,9 +513,11 @@ def other_workload(args):
         cfg = {"workload": "WoodBerry DTC-GPC Monte-Carlo, nit=200, sharded by candidate", "candidates": Cc,
                "draws": D}
     Cg = len(N2)
-    # config 3's work varies ~100x over the grid: snake-deal by the a-priori latency estimate;
-    # the others strided (every rank gets the same mix of candidates)
-    sidx, owners = plan_shards(N2, Nu, l, world, rank, keyed=args.workload == "shell7x5", nu=sc.nu)
+    # config 3's work varies ~100x over the grid: whole (N2, Nu) cells packed by their measured
+    # one-GPU times (mpct.dist.plan_cells_lpt, the committed mpct/config3_cells.json); the others
+    # strided (every rank gets the same mix of candidates)
+    sidx, owners = plan_shards(N2, Nu, l, world, rank, keyed="cells" if args.workload == "shell7x5" else False,
+                               nu=sc.nu)
     sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, sidx)
     C = sidx.size
     S = C * nref

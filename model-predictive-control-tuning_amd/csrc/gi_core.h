@@ -64,6 +64,9 @@ struct GIState {
   int q;            // active-set size (wave-uniform)
   int nrot;         // rotations applied to J since it was last built from R^-1 (uniform)
   bool jinit;       // J holds a factorisation consistent with the active set (uniform)
+#ifdef MPCT_DIAG
+  int diag = 0;     // planted faults of the diagnostic build (DevOpts::diag)
+#endif
 };
 
 template <int MAXM>

@@ -211,6 +211,9 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? kWaves16 : 1)
 
   GIState<MAXM> gis;  // active-set factorisation carried across the steps (warm start)
   gi_reset<MAXM>(gis);
+#ifdef MPCT_DIAG
+  gis.diag = o.diag;
+#endif
   RegFactors rf;      // M <= 16 class: J in VGPRs, B = R_A^-1 in LDS (gpc_qp16.h), valid once gis.jinit
   FOR4(r, rf.J[r] = 0.0;);
   rf.sB = lds + L.gb;

@@ -129,8 +129,14 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
+#ifdef MPCT_DIAG
+        if (!(S.diag & kDiagSkipWarmDrop))
+#endif
         gi_drop<MAXM>(S, sJT, sRA, M, kd, BoxMark{});
-        ++it;
+        if (++it >= maxit) {  // a drop shrinks the set: only a logic slip reaches the cap (gpc_qp16.h)
+          *st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
       }
       if (!row) xm = 0.0;
     }
@@ -199,6 +205,11 @@ __device__ __forceinline__ int gi_qp(const QPBufs& Q, int M, int Nu, const RowCo
       if (full) {
         gi_add<MAXM>(S, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, BoxMark{});
         PSTAMP(PROF_QADD);
+        break;
+      }
+      if (kdrop >= S.q) {  // t1 or t2 NaN: no lane attains the ratio test (a non-finite state)
+        *st |= MPCT_ST_NONFINITE_;
+        infeas = true;
         break;
       }
       gi_drop<MAXM>(S, sJT, sRA, M, kdrop, BoxMark{});

@@ -50,9 +50,17 @@ struct RegFactors {
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
 // candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
 constexpr int kBS = 16;
+#ifndef MPCT_DROP_MERGE
+#define MPCT_DROP_MERGE 0
+#endif
 // Drops keep R_A and its Givens chain: drops derived from B alone, as the band kernel's (DESIGN §11
 // round 5), measured the same at 4096 candidates and 1 % slower on the heaviest 256 here (DESIGN §6
-// round 5): the metric's drops average three rotations, and J's register rotations dominate them
+// round 5): the metric's drops average three rotations, and J's register rotations dominate them.
+// Round 6 (profiles/r06a_drop_ab.txt): the column / row shifts as one parallel pass of the wave
+// (all loads, then all stores) and the Givens chain with R_A's row and B's column carried in
+// registers, (a, c) by readlane and no hand-off per rotation, were 3-12 % slower at 4096 candidates
+// and on the heaviest 256: both add live values to a step loop at the 128-VGPR budget, whose
+// allocator answers with 2-5 more step-loop invariants spilled and reloaded every step
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
@@ -285,9 +293,21 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);
   lds_sync();  // R_A and B columns written by the adds
+#if MPCT_DROP_MERGE
+  // R_A loses column kd (lanes = rows) and B loses row kd (lanes = columns) in one loop, before the
+  // rotations: removing a row of B commutes with rotating its columns (B G' minus row kd), so the
+  // two serial shift chains run side by side instead of one after the other
+  if (lane < q) {
+    for (int w = kd; w < q - 1; ++w) {
+      sRA[lane * M + w] = sRA[lane * M + w + 1];
+      sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
+    }
+  }
+#else
   if (lane < q) {  // remove column kd (lanes = rows of row block 0)
     for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
   }
+#endif
   {
     const double un = lane_next<16>(S.uw);
     const int wn = lane_next_i<16>(S.ww);
@@ -319,10 +339,12 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
     }
     lds_sync();
   }
+#if !MPCT_DROP_MERGE
   // row kd of B G' leaves (lanes = columns)
   if (lane < q - 1) {
     for (int w = kd; w < q - 1; ++w) sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
   }
+#endif
   const int qn = q - 1;
   if (i == qn) {
     S.uw = 0.0;
@@ -378,12 +400,16 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
       xout = xu;
       return 0;
     }
+    PSTAMP(PROF_QWENTRY);
     if (S.q == 0) {
       S.jinit = false;  // nothing retained: restart from R^-1 when the first constraint enters
     } else {
       if (!S.jinit || S.nrot >= rebuild * M) {
         // rebuild J and B for the retained set from R^-1, re-adding it in order
         const int qq = S.q;
+#ifdef MPCT_PROFILE
+        pacc[PROF_QWREADD] += (unsigned long long)qq * kProfCount;
+#endif
         gi16_load_rinv<PACKED>(S, F, sRi, M);
         S.q = 0;
         for (int v = 0; v < qq; ++v) {
@@ -404,6 +430,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         }
         S.nrot = 0;
       }
+      PSTAMP(PROF_QWREB);
       lds_sync();
       // equality-constrained solve on the retained set, dropping negative multipliers:
       // w = R_A^-T c = B'c, x = x_u + J(:,0:q) w, lambda = R_A^-1 w = B w.
@@ -416,6 +443,7 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         const double g2 = __shfl(s[2], src, kWave), g3 = __shfl(s[3], src, kWave);
         c = i < S.q ? -sel4v_v(g0, g1, g2, g3, S.ww & 3) : 0.0;
       }
+      PSTAMP(PROF_QWGATH);
       for (;;) {
         const int q = S.q;
         if (q == 0) {
@@ -441,17 +469,30 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
         double lmin = i < q ? lam : INFINITY;
         int kd = i;
         qargmin<16>(lmin, kd, 0);
+        PSTAMP(PROF_QWSOLVE);
         if (!(lmin < 0.0)) break;
 #ifdef MPCT_PROFILE
-        pacc[PROF_QROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
+        pacc[PROF_QWROT] += (unsigned long long)(S.q - 1 - kd) * kProfCount;
 #endif
-        gi16_drop(S, F, sRA, M, kd, mark);
-        {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
-          const double cn = lane_next<16>(c);
-          if (i >= kd && i < q - 1) c = cn;
-          else if (i == q - 1) c = 0.0;
+#ifdef MPCT_DIAG
+        if (!(S.diag & kDiagSkipWarmDrop))
+#endif
+        {
+          gi16_drop(S, F, sRA, M, kd, mark);
+          {  // c follows the ids: entries kd + 1 .. q - 1 move down one lane
+            const double cn = lane_next<16>(c);
+            if (i >= kd && i < q - 1) c = cn;
+            else if (i == q - 1) c = 0.0;
+          }
         }
-        ++it;
+        PSTAMP(PROF_QWDROP);
+        // every drop shrinks the set, so the loop ends within q passes; the cap turns a logic slip
+        // that stops the shrinking into MPCT_ST_QP_MAXITER instead of a wave that never retires
+        // (the release build of commit 0272c65 hung the GPU that way).  it <= 2M < maxit here
+        if (++it >= maxit) {
+          *st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
       }
       if (!row) xm = 0.0;
     }
@@ -522,6 +563,11 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
       if (full) {
         add(p, d, beta, zm, jq, rk, upm);
         PSTAMP(PROF_QADD);
+        break;
+      }
+      if (kdrop >= S.q) {  // t1 or t2 NaN: no lane attains the ratio test (a non-finite state)
+        *st |= MPCT_ST_NONFINITE_;
+        infeas = true;
         break;
       }
 #ifdef MPCT_PROFILE

@@ -152,6 +152,9 @@ __global__ void __launch_bounds__(64, 4)
   const double* psy = sc.yref + (long long)si * nit;
   GIState<16> gis;
   gi_reset<16>(gis);
+#ifdef MPCT_DIAG
+  gis.diag = o.diag;
+#endif
   RegFactors rf;
   FOR4(r, rf.J[r] = 0.0;);
   rf.sB = lds + L.gb;

@@ -511,6 +511,9 @@ __global__ void __launch_bounds__(64, 1)
   const BandMark mark{sbits, base};
   GIState<MAXM> gis;
   gi_reset<MAXM>(gis);
+#ifdef MPCT_DIAG
+  gis.diag = o.diag;
+#endif
 #ifdef MPCT_DEBUG_BAND
   int dbg_t = -1, dbg_reb = 0, dbg_pol = 0, dbg_git = 0;
 #endif
@@ -771,6 +774,7 @@ __global__ void __launch_bounds__(64, 1)
       }
       lds_sync();
       double x = row ? xu : 0.0;
+      int nd = 0;  // drops of this solve: each shrinks the set, so at most q <= Mz of them
       for (;;) {
         const int q = gis.q;
         if (q == 0) {
@@ -808,8 +812,15 @@ __global__ void __launch_bounds__(64, 1)
         int kd = lane;
         qargmin<MAXM>(lmin, kd);
         if (!(lmin < 0.0)) break;
+#ifdef MPCT_DIAG
+        if (!(gis.diag & kDiagSkipWarmDrop))
+#endif
         band_drop_b(gis, sJT, sBT, Mz, kd, mark, snv, sd);
         ++it;
+        if (++nd > Mz) {  // only a logic slip that stops the set shrinking gets here (gpc_qp16.h)
+          st |= MPCT_ST_QP_MAXITER_;
+          break;
+        }
       }
       return row ? x : 0.0;
     };
@@ -905,6 +916,11 @@ __global__ void __launch_bounds__(64, 1)
         if (full) {
           gi_add<MAXM>(gis, sJT, sRA, sd, Mz, p, dk, beta, zm, upm, row, mark, RANone{}, BandBAdd{sBT, rk});
           PSTAMP(PROF_QADD);
+          break;
+        }
+        if (kdrop >= gis.q) {  // t1 or t2 NaN: no lane attains the ratio test (a non-finite state)
+          st |= MPCT_ST_NONFINITE_;
+          infeas = true;
           break;
         }
         band_drop_b(gis, sJT, sBT, Mz, kdrop, mark, snv, sd);

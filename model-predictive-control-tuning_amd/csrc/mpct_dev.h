@@ -129,7 +129,15 @@ struct DevScenario {
 struct DevOpts {
   int open_loop, want_traj, max_qp_iter;
   double feas_tol;
+#ifdef MPCT_DIAG
+  // diagnostic build only: planted kernel faults (kDiagSkipWarmDrop: the QPs' warm start computes
+  // its drop but never applies it, so only the warm loop's own cap can end it)
+  int diag;
+#endif
 };
+#ifdef MPCT_DIAG
+constexpr int kDiagSkipWarmDrop = 1;
+#endif
 
 // staging row of an ordered launch: the fields the caller asked for, in the order
 // J1 [my] | j21 [my] | j22 [my] | Jnu [nu] | status | qp_iters (one double each); -1 = not staged
@@ -177,8 +185,13 @@ inline StageRow stage_row(const DevResult& o, int my, int nu) {
 
 // section ids of the diagnostic in-kernel stamps
 enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, PROF_OPENLOOP,
-       PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_QWARM, PROF_QROT, PROF_N = 14 };
-// PROF_QROT: a count only (the drops' Givens rotations, gpc_qp16.h), no cycles
+       PROF_QCHECK, PROF_QD, PROF_QR, PROF_QADD, PROF_QDROP, PROF_QWARM, PROF_QROT, PROF_QWENTRY, PROF_QWREB,
+       PROF_QWGATH, PROF_QWSOLVE, PROF_QWDROP, PROF_QWROT, PROF_QWREADD, PROF_N = 21 };
+// PROF_QROT: a count only (the drops' Givens rotations, gpc_qp16.h), no cycles.  The warm start of
+// gpc_qp16.h: PROF_QWENTRY the entry test of an infeasible x_u, PROF_QWREB the
+// J / B rebuild from R^-1, PROF_QWGATH the slacks' gather, PROF_QWSOLVE one pass of the equality
+// solve, PROF_QWDROP one drop of a negative multiplier; PROF_QWARM closes what is left.
+// PROF_QWROT / PROF_QWREADD: counts only (the warm drops' Givens rotations, the rebuild's re-adds)
 // nmpc_kernel.hip's sections (same slots): the prediction with tangents and its streamed QR when
 // it starts an iteration, R^-1 and the unconstrained step, the QP, the Anderson candidate's
 // prediction, the full-step (alpha = 1) trial prediction, the shorter Armijo trials (tangent-free),

@@ -1038,6 +1038,10 @@ static DevOpts make_opts(const mpct_opts* o) {
   d.want_traj = o ? o->want_traj : 0;
   d.max_qp_iter = o ? o->max_qp_iter : 0;
   d.feas_tol = (o && o->feas_tol > 0) ? o->feas_tol : 1e-10;
+#ifdef MPCT_DIAG
+  const char* e = getenv("MPCT_DIAG_SKIP_WARM_DROP");
+  d.diag = (e && *e && atoi(e) != 0) ? kDiagSkipWarmDrop : 0;
+#endif
   return d;
 }
 
@@ -1106,13 +1110,14 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
     (void)hipStreamSynchronize(stream);
     (void)hipMemcpy(hp.data(), dprof, sizeof(unsigned long long) * S * PROF_N, hipMemcpyDeviceToHost);
     (void)hipFree(dprof);
-    // low 48 bits: cycles, high 16: executions of the section (wave_ops.h PSTAMP)
-    const unsigned long long cmask = (1ull << 48) - 1;
+    // low 40 bits: cycles, high 24: executions of the section (wave_ops.h PSTAMP, kProfCountShift)
+    constexpr int kProfCountShift = 40;
+    const unsigned long long cmask = (1ull << kProfCountShift) - 1;
     double sum[PROF_N] = {0}, mx[PROF_N] = {0}, cnt[PROF_N] = {0};
     for (long long i = 0; i < S; ++i)
       for (int k = 0; k < PROF_N; ++k) {
         sum[k] += (double)(hp[i * PROF_N + k] & cmask);
-        cnt[k] += (double)(hp[i * PROF_N + k] >> 48);
+        cnt[k] += (double)(hp[i * PROF_N + k] >> kProfCountShift);
         mx[k] = std::max(mx[k], (double)(hp[i * PROF_N + k] & cmask));
       }
     if (const char* po = getenv("MPCT_PROF_OUT")) {  // per simulation, raw (tools/latency_model.py)
@@ -1123,9 +1128,11 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
       }
     }
     const char* gpc_nm[PROF_N] = {"prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update",
-                                  "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations"};
+                                  "open_loop", "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm",
+                                  "qp.rotations", "qp.w.entry", "qp.w.rebuild", "qp.w.gather", "qp.w.solve",
+                                  "qp.w.drop", "qp.w.rotations", "qp.w.readds"};
     const char* nmpc_nm[PROF_N] = {"full_pass", "rinv+step", "qp", "anderson_pass", "ls_full_pass", "ls_trials",
-                                   "plant_rk4", "other", "-", "-", "-", "-", "-", "-"};
+                                   "plant_rk4", "other", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-"};
     const char** nm = s->nmpc ? nmpc_nm : gpc_nm;
     fprintf(stderr, "[mpct profile] mean / max cycles and mean executions per simulation over %lld sims\n", S);
     for (int k = 0; k < PROF_N; ++k)

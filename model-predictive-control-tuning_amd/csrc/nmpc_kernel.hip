@@ -512,6 +512,11 @@ __global__ void __launch_bounds__(64, 1)
             gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, mark);
             break;
           }
+          if (kdrop >= gis.q) {  // t1 or t2 NaN: no lane attains the ratio test (a non-finite state)
+            st |= MPCT_ST_NONFINITE_;
+            infeas = true;
+            break;
+          }
           gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, mark);
           if (git >= maxit) break;
         }

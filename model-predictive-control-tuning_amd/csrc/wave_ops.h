@@ -302,9 +302,12 @@ __device__ __forceinline__ void qargmin(double& v, int& id, int shift = -1) {
 }
 
 #ifdef MPCT_PROFILE
-// diagnostic build: section k's cycles in the low 48 bits of pacc[k], the number of times the
-// section ended in the high 16 (tools/latency_model.py divides one by the other)
-constexpr unsigned long long kProfCount = 1ull << 48;
+// diagnostic build: section k's cycles in the low 40 bits of pacc[k] (1.1e12 cycles, minutes of one
+// simulation), the number of times the section ended in the high 24 (tools/latency_model.py divides
+// one by the other).  24 bits hold the band and NMPC kernels' counts too: a heavy config-3
+// simulation ends its QP sections ~1e5 times, past the 16 bits of the first layout
+constexpr int kProfCountShift = 40;
+constexpr unsigned long long kProfCount = 1ull << kProfCountShift;
 // ProfAcc: the section words live in one 64-bit VGPR pair, lane k holding word k.  The SGPR array
 // of PROF_N words (ProfAccS, the first form) was copied whole at every loop back-edge of the metric
 // kernel's step loop (28 s_mov per QP iteration), which inflated the sections it was measuring.

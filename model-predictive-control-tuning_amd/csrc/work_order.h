@@ -46,9 +46,14 @@ int unpermute_results(const WorkOrder& wo, long long C, int nref, int my, int nu
 // MPCT_ST_NOT_RUN, 0 iterations; enqueue before the class launches, which overwrite the records
 // of the slots they simulate, so a slot that no launch claims cannot pass for a result
 int prefill_results(const DevResult& out, long long S, int my, int nu, hipStream_t stream, std::string* err);
-// diagnostic: with MPCT_DIAG_DROP_LAUNCH=k in the environment the k-th class launch of every batch
-// is not issued (tests plant the dispatch fault that the prefill must expose); unset, never true
+// diagnostic build only (-DMPCT_DIAG, csrc/libmpct_diag.so): with MPCT_DIAG_DROP_LAUNCH=k in the
+// environment the k-th class launch of every batch is not issued (tests plant the dispatch fault
+// that the prefill must expose).  The release library has no fault hook: always false
+#ifdef MPCT_DIAG
 bool diag_drop_launch(int k);
+#else
+inline bool diag_drop_launch(int) { return false; }
+#endif
 
 // after the launch(es) that read *perm: later sorts wait for them before rewriting the buffer
 void order_mark_used(WorkOrder& wo, hipStream_t stream);

@@ -602,10 +602,12 @@ __global__ void prefill_kernel(DevResult out, long long S, int my, int nu) {
   prefill_slot(out, s, S, my, nu);
 }
 
+#ifdef MPCT_DIAG
 bool diag_drop_launch(int k) {
   const char* e = getenv("MPCT_DIAG_DROP_LAUNCH");
   return e && *e && atoi(e) == k;
 }
+#endif
 
 int prefill_results(const DevResult& out, long long S, int my, int nu, hipStream_t stream, std::string* err) {
   if (S <= 0) return 0;

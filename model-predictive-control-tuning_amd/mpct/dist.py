@@ -12,6 +12,9 @@ backend-agnostic (torch.distributed with "nccl" = RCCL on the GPU box, "gloo" in
 """
 from __future__ import annotations
 
+import json
+import os
+
 import numpy as np
 import torch
 
@@ -116,11 +119,111 @@ def rank_candidates(costs: torch.Tensor, weights: torch.Tensor, C: int | None = 
     return torch.argsort(s, stable=True)
 
 
-def plan_shards(N2, Nu, lam, world: int, rank: int, keyed: bool = False, nu: int = 3):
+# measured one-GPU time of every config-3 cell alone (tools/shard_balance.py --cells): the (N2, Nu)
+# cells of mpct.scenarios.config3_grid with 1024 lambda draws each, whole and in two halves
+CELL_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "config3_cells.json")
+
+
+def load_cell_table(path: str = CELL_TABLE) -> dict:
+    """{(N2, Nu): {"ms": whole cell, "half_ms": [half 0, half 1], "n": draws}} from the committed
+    table (tools/shard_balance.py --cells writes it)."""
+    with open(path) as f:
+        tj = json.load(f)
+    return {(int(c["N2"]), int(c["Nu"])): dict(ms=float(c["ms"]), half_ms=[float(x) for x in c["half_ms"]],
+                                               n=int(c["n"])) for c in tj["cells"]}
+
+
+def cell_halves(idx, work):
+    """The two halves of one cell's candidates `idx` (ascending): sorted by descending estimated
+    work (ties by index) and dealt alternately, so both halves get the same share of the heavy draws."""
+    order = np.asarray(idx)[np.argsort(-np.asarray(work, dtype=float), kind="stable")]
+    return np.sort(order[0::2]), np.sort(order[1::2])
+
+
+# overlap of a shard's cells on one GPU: the cells' class launches run side by side and their
+# alone-times are mostly latency, not occupancy, so a shard takes about its heaviest cell plus a
+# fraction of the others.  Least squares over the 48 shards of six measured plans
+# (profiles/r06b_shard_plans.json): 0.873 x heaviest + 0.470 x the rest (rms 12 ms), i.e. the rest
+# at 0.54 of the heaviest's weight
+SHARD_OVERLAP = 0.54
+# cells costlier than this are split into their two halves before packing (None: an even share,
+# total / world).  Splitting measured no better: a half's alone-time is most of its cell's (the
+# heaviest cell 129 ms whole, 119 + 93 ms as halves; r06a_config3_cells.json), so halves add load
+SPLIT_MS = None
+
+
+def plan_cells_lpt(N2, Nu, lam, world: int, table: dict | None = None, nu: int = 3, split_ms: float | None = SPLIT_MS,
+                   beta: float = SHARD_OVERLAP):
+    """Config 3's split from measured cell times.  The candidates are grouped
+    into their (N2, Nu) cells, every cell costed by the committed table (a partial cell pro rata by
+    its count; a cell the table lacks by band_work_estimate, scaled by the table's median ms per
+    estimate unit).  A cell costlier than split_ms (None: an even share, total / world) is split
+    into two halves (cell_halves; their own measured times for a whole table cell).  Then greedy
+    longest-processing-time packing under the shard model of SHARD_OVERLAP: a shard's predicted
+    time is its heaviest unit plus beta times the rest (beta = 1: plain LPT on sums); units by
+    descending time (ties by cell), each to the rank whose prediction it raises least (ties by
+    rank).  Every rank scores few cells, so its class launches stay full, and the predicted times
+    balance.  Deterministic: every rank derives the same owners.
+
+    Returns (owners, loads): owners[r] = rank r's candidate indices, ascending, padded to one size
+    with distinct sentinel indices >= C (gather_costs scatters them past the grid); loads[r] = the
+    predicted ms of rank r."""
+    N2 = np.asarray(N2)
+    Nu = np.asarray(Nu)
+    C = N2.size
+    table = load_cell_table() if table is None else table
+    work = band_work_estimate(N2, Nu, lam, nu)
+    keys = sorted(set(zip(N2.tolist(), Nu.tolist())))
+    groups = {k: np.nonzero((N2 == k[0]) & (Nu == k[1]))[0] for k in keys}
+    scale = float(np.median([t["ms"] / np.sum(band_work_estimate(np.full(t["n"], k[0]), np.full(t["n"], k[1]),
+                                                                   np.ones((t["n"], nu)), nu))
+                             for k, t in table.items()])) if table else 1.0
+    cost = {}
+    for k, idx in groups.items():
+        t = table.get(k)
+        cost[k] = t["ms"] * idx.size / t["n"] if t else scale * float(np.sum(work[idx]))
+    lim = sum(cost.values()) / world if split_ms is None else split_ms
+    units = []  # (ms, cell rank for ties, half, indices)
+    for ci, k in enumerate(keys):
+        idx = groups[k]
+        t = table.get(k)
+        if cost[k] > lim and idx.size >= 2:
+            halves = cell_halves(idx, work[idx])
+            for h, part in enumerate(halves):
+                ms = t["half_ms"][h] * 2 * part.size / t["n"] if t else cost[k] * part.size / idx.size
+                units.append((ms, ci, h, part))
+        else:
+            units.append((cost[k], ci, 0, idx))
+    units.sort(key=lambda u: (-u[0], u[1], u[2]))
+    top = [0.0] * world   # heaviest unit of each rank
+    rest = [0.0] * world  # the sum of its others
+    mine = [[] for _ in range(world)]
+    for ms, _, _, idx in units:
+        new = [max(top[r], ms) + beta * (rest[r] + min(top[r], ms)) for r in range(world)]
+        r = int(np.argmin(new))
+        rest[r] += min(top[r], ms)
+        top[r] = max(top[r], ms)
+        mine[r].append(idx)
+    loads = [top[r] + beta * rest[r] for r in range(world)]
+    owners = [np.sort(np.concatenate(m)) if m else np.zeros(0, np.int64) for m in mine]
+    n = max(o.size for o in owners)
+    nxt = C
+    for r in range(world):
+        pad = n - owners[r].size
+        owners[r] = np.concatenate([owners[r], np.arange(nxt, nxt + pad)]).astype(np.int64)
+        nxt += pad
+    return owners, loads
+
+
+def plan_shards(N2, Nu, lam, world: int, rank: int, keyed: bool | str = False, nu: int = 3):
     """The candidates rank scores and the owners table gather_costs needs: strided shards (owners
-    None), or, keyed (config 3, whose per-simulation latency varies ~100x over the grid), the snake
-    deal of shard_indices_keyed by band_work_estimate with every rank's owners (identical on every
-    rank, so the gathered rows land in the grid's order).  Returns (idx, owners)."""
+    None); keyed="cells" (config 3, bench.py): plan_cells_lpt over the committed cell-time table;
+    keyed=True: round 3's snake deal of shard_indices_keyed by band_work_estimate (kept for the
+    shard-balance comparison: measured slower).  The owners are identical on every
+    rank, so the gathered rows land in the grid's order.  Returns (idx, owners)."""
+    if keyed == "cells":
+        owners, _ = plan_cells_lpt(N2, Nu, lam, world, nu=nu)
+        return owners[rank], owners
     if keyed:
         work = band_work_estimate(N2, Nu, lam, nu)
         owners = [shard_indices_keyed(work, world, k) for k in range(world)]

@@ -102,21 +102,47 @@ def test_shard_indices_cover_grid_and_match_library(built):
                 np.testing.assert_array_equal(shard_candidates(C, W, r), parts[r][parts[r] < C])
 
 
-def test_config3_strided_shards_are_balanced():
-    """Config 3's grid is cell-ordered (1024 lambda draws per (N2, Nu) cell, N2-major): the
-    contiguous split of round 2 gave rank r of 8 exactly N2 = CONFIG3_N2[r]; the strided split gives
-    every rank 128 draws of every cell, so the per-rank work model (sum of N2 * (3 Nu + 1) over the
-    shard, the output-row scan of DESIGN §7) is equal on every rank."""
-    from mpct.dist import shard_indices
-    from mpct.scenarios import config3_grid
+def test_config3_plans_against_the_cell_table():
+    """Config 3's grid is cell-ordered (1024 lambda draws per (N2, Nu) cell, N2-major).  Against the
+    committed one-GPU time of every cell (mpct/config3_cells.json, tools/shard_balance.py --cells;
+    VERDICT r5 item 1: a measured table, not a work model): the contiguous split of round 2 gives
+    rank r of 8 one N2 and a predicted max/mean far from 1; the cell plan (plan_cells_lpt) gives
+    every rank whole cells, covers the grid exactly once, pads with distinct sentinels and balances
+    the predicted shard times; the strided split hands every rank 1/W of every cell (the split of
+    the other workloads)."""
+    from mpct.dist import SHARD_OVERLAP, load_cell_table, plan_cells_lpt, shard_indices
+    from mpct.scenarios import CONFIG3_N2, CONFIG3_NU, config3_grid
 
+    table = load_cell_table()
+    assert set(table) == {(n, u) for n in CONFIG3_N2 for u in CONFIG3_NU}
+    assert all(t["ms"] > 0 and len(t["half_ms"]) == 2 and t["n"] == 1024 for t in table.values())
     N2, Nu, D, L = config3_grid(1024)
-    work = N2.astype(float) * (3 * Nu + 1)
+    C = N2.size
+
+    def pred(idx):  # the packing model: heaviest cell + SHARD_OVERLAP x the rest (pro rata)
+        idx = idx[idx < C]
+        ts = sorted((table[k]["ms"] * np.count_nonzero((N2[idx] == k[0]) & (Nu[idx] == k[1])) / 1024
+                     for k in set(zip(N2[idx].tolist(), Nu[idx].tolist()))), reverse=True)
+        return ts[0] + SHARD_OVERLAP * sum(ts[1:])
+
     for W in (2, 4, 8):
-        per_rank = [work[shard_indices(N2.size, W, r)].sum() for r in range(W)]
-        assert max(per_rank) / np.mean(per_rank) == 1.0
-        contiguous = [work[r * N2.size // W:(r + 1) * N2.size // W].sum() for r in range(W)]
-        assert max(contiguous) / np.mean(contiguous) > 1.3
+        owners, loads = plan_cells_lpt(N2, Nu, L, W)
+        allc = np.concatenate(owners)
+        assert len({o.size for o in owners}) == 1                     # equal sizes for the all-gather
+        np.testing.assert_array_equal(np.sort(allc[allc < C]), np.arange(C))
+        assert np.unique(allc).size == allc.size                       # distinct sentinels
+        for o, ld in zip(owners, loads):
+            live = o[o < C]
+            cells = set(zip(N2[live].tolist(), Nu[live].tolist()))
+            assert live.size == 1024 * len(cells)                      # whole cells only
+            assert abs(pred(o) - ld) < 1e-6 * ld
+        assert max(loads) / np.mean(loads) < 1.06
+        contiguous = [pred(np.arange(r * C // W, (r + 1) * C // W)) for r in range(W)]
+        assert max(contiguous) / np.mean(contiguous) > 1.1
+        assert max(loads) < max(contiguous)
+        for r in range(W):
+            sh = shard_indices(C, W, r)
+            assert all(np.count_nonzero((N2[sh] == n) & (Nu[sh] == u)) == 1024 // W for (n, u) in table)
 
 
 # ---- bench.py's config-3 and config-4 multi-rank logic (VERDICT r4 item 6): mpct.dist.plan_shards
@@ -187,7 +213,7 @@ def _cfg_worker(rank, world, port, cfg, q):
         else:
             N2, Nu, d, l = _c4_grid()
             costs, nref, w = _c4_costs, C4_DRAWS, np.ones(2)
-        idx, owners = plan_shards(N2, Nu, l, world, rank, keyed=cfg == "shell7x5")
+        idx, owners = plan_shards(N2, Nu, l, world, rank, keyed="cells" if cfg == "shell7x5" else False)
         sN2, sNu, sd, sl = pad_shard(N2, Nu, d, l, idx)
         J = torch.from_numpy(costs(sN2, sNu, sd, sl))
         g, order = gather_and_rank(J, idx.size, nref, torch.tensor(w, dtype=torch.float64), len(N2), owners=owners)
@@ -198,12 +224,13 @@ def _cfg_worker(rank, world, port, cfg, q):
 
 @pytest.mark.parametrize("cfg", ["shell7x5", "dtc-mc"])
 def test_two_rank_bench_workloads(built, cfg):
-    """bench.py's multi-rank paths of configs 3 and 4 at world size 2 over gloo: config 3's keyed
-    owners (band_work_estimate snake deal, measured disturbances in every simulation) and config 4's
-    draws co-located on their candidate's rank with the worst case over draws.  Every rank holds
+    """bench.py's multi-rank paths of configs 3 and 4 at world size 2 over gloo: config 3's cell-plan
+    owners (plan_cells_lpt over the committed cell table: whole cells per rank, unequal live counts
+    padded with sentinels; measured disturbances in every simulation) and config 4's draws
+    co-located on their candidate's rank with the worst case over draws.  Every rank holds
     bit-identical gathered records equal to the single-process costs, NaN sentinel padding, and the
     same ranking as a single process."""
-    from mpct.dist import band_work_estimate, shard_indices_keyed
+    from mpct.dist import plan_cells_lpt
     from mpct.scenarios import SHELL7_W
 
     world = 2
@@ -221,11 +248,11 @@ def test_two_rank_bench_workloads(built, cfg):
     if cfg == "shell7x5":
         N2, Nu, d, l = _c3_subgrid()
         ref, w = _c3_costs(N2, Nu, d, l), SHELL7_W
-        owners = [shard_indices_keyed(band_work_estimate(N2, Nu, l), world, k) for k in range(world)]
+        owners, _ = plan_cells_lpt(N2, Nu, l, world)
         for rank, idx, own, g, order in got:
             np.testing.assert_array_equal(idx, owners[rank])
             assert own == [o.tolist() for o in owners]
-        # the keyed deal is not the strided one here (it is the point of the test)
+        # not the strided split (it is the point of the test)
         assert not np.array_equal(owners[0][owners[0] < len(N2)], np.arange(0, len(N2), 2))
     else:
         N2, Nu, d, l = _c4_grid()
@@ -233,7 +260,7 @@ def test_two_rank_bench_workloads(built, cfg):
         ref, w = sims.max(axis=1), np.ones(2)
         assert np.all(sims.max(axis=1) > sims.min(axis=1))   # the draws differ: amax selects
     C = len(N2)
-    per = -(-C // world)
+    per = got[0][1].size  # the shards' common (padded) size
     ref_order = np.argsort(ref @ w, kind="stable")
     for rank, idx, own, g, order in got:
         assert g.shape == (world * per, ref.shape[1])

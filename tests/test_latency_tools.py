@@ -52,6 +52,33 @@ def test_latency_model_synthetic(tmp_path):
     assert rep["model_cycles"] <= rep["measured_cycles"]
 
 
+def test_latency_model_warm_split(tmp_path):
+    """r06 profile layout: 21 words per simulation, counts in the high 24 bits,
+    the warm start priced per section (entry, rebuild + re-adds, gather, solve passes, drops + their
+    rotations) and the old qp.warm word a near-empty remainder."""
+    names = SECTIONS + ["qp.w.entry", "qp.w.rebuild", "qp.w.gather", "qp.w.solve", "qp.w.drop", "qp.w.rotations",
+                        "qp.w.readds"]
+    words = np.zeros((4, len(names)), dtype=np.uint64)
+    for k, name in enumerate(names):
+        execs = 500 if k < 7 else (700 if name == "qp.check" else 100)
+        words[:, k] = np.uint64(1000 * execs) | (np.uint64(execs) << np.uint64(40))
+    prof = tmp_path / "prof21.bin"
+    words.tofile(prof)
+    out = tmp_path / "model21.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "latency_model.py"), str(_probe(tmp_path)),
+                        str(prof), "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(out.read_text())
+    sec = rep["sections"]
+    assert sec["qp.check"]["executions"] == 200.0          # 40-bit split decoded
+    assert sec["qp.warm"]["model"] == 0                     # split into qp.w.*
+    for name in ("qp.w.entry", "qp.w.rebuild", "qp.w.gather", "qp.w.solve", "qp.w.drop"):
+        assert sec[name]["model"] > 0, name
+    # the warm drops and the rebuild carry their counted rotations / re-adds on top of the base chain
+    assert sec["qp.w.drop"]["model"] > sec["qp.w.drop"]["chain_cycles"] * 100
+    assert sec["qp.w.rebuild"]["model"] > sec["qp.w.rebuild"]["chain_cycles"] * 100
+
+
 def test_section_isa_counts(tmp_path):
     from section_isa import section_counts
 

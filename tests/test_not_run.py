@@ -7,8 +7,9 @@ every slot is prefilled with MPCT_ST_NOT_RUN and NaN costs before the class laun
 The reference treats a failed sim as an error, never as a value (VNS2.m:151-163, GAM_fun.m:82-84).
 
 GPU: the full config-3 and config-5 grids and a mixed-horizon Shell 3x3 batch leave no NOT_RUN
-bit; a planted fault (MPCT_DIAG_DROP_LAUNCH: one class launch not issued) comes back NOT_RUN with
-NaN costs on exactly the dropped class's slots, and objectives.failed() rejects them."""
+bit; a planted fault (MPCT_DIAG_DROP_LAUNCH: one class launch not issued, in the diagnostic
+library libmpct_diag.so) comes back NOT_RUN with NaN costs on exactly the dropped class's slots,
+and objectives.failed() rejects them."""
 import os
 
 import numpy as np
@@ -49,18 +50,17 @@ def gpu(built, has_gpu):
 
 def _mixed_shell3x3():
     """Shell 3x3 with nu_max = 15: every QP-size class (16 / 32 / 64) of the general kernel, the
-    small-plant kernel's class, padding and bad horizons, three VNS reference sets."""
-    from mpct.scenarios import shell3x3, vns_step_refs
+    small-plant kernel's class, padding and bad horizons, three VNS reference sets (the fault
+    tests' "mixed" batch, tests/diag_child.py)."""
+    import sys
 
-    rng = np.random.default_rng(11)
-    C = 300
-    N2 = rng.integers(16, 41, size=C).astype(np.int32)
-    Nu = np.minimum(rng.integers(1, 16, size=C), N2).astype(np.int32)
-    N2[:3], Nu[:3] = (0, 41, 5), (2, 2, 9)  # skipped, N2 > n2_max, Nu > N2
-    d = 10.0 ** rng.uniform(-3, 0, size=(C, 3))
-    l = 10.0 ** rng.uniform(-3, -1, size=(C, 3))
-    sc, r, yref = shell3x3(n2_max=40, nu_max=15, nit=120)
-    return sc, N2, Nu, d, l, r, vns_step_refs(3, 120)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from diag_child import fault_cases
+    from mpct.scenarios import shell3x3
+
+    sc, N2, Nu, d, l, refs, _, _ = fault_cases()["mixed"]
+    _, r, _ = shell3x3(n2_max=40, nu_max=15, nit=120)
+    return sc, N2, Nu, d, l, r, refs
 
 
 @pytest.mark.gpu
@@ -92,33 +92,33 @@ def test_no_slot_left_unsimulated(gpu):
 
 
 @pytest.mark.gpu
-def test_dropped_class_launch_reports_not_run(gpu, monkeypatch):
-    """A planted dispatch fault: with MPCT_DIAG_DROP_LAUNCH=k the k-th class launch of the batch is
-    not issued.  Exactly the slots of its class come back NOT_RUN with NaN costs and 0 iterations;
-    every other slot equals the fault-free run bit for bit; failed() rejects the dropped ones."""
+def test_dropped_class_launch_reports_not_run(gpu, tmp_path):
+    """A planted dispatch fault: with MPCT_DIAG_DROP_LAUNCH=k the diagnostic library
+    (libmpct_diag.so, -DMPCT_DIAG; the release library has no such hook) does not issue
+    the k-th class launch of the batch.  Exactly the slots of its class come back NOT_RUN with NaN
+    costs and 0 iterations; every other slot equals the release library's fault-free run bit for
+    bit; failed() rejects the dropped ones."""
     from mpct import _lib
-    from mpct.engine import eval_batch
     from mpct.objectives import failed
+    from test_qp_caps import run_diag, run_release
 
     sc, N2, Nu, d, l, r, refs = _mixed_shell3x3()
     M = 3 * Nu.astype(int)
     valid = (N2 > 0) & (N2 <= 40) & (Nu <= N2)
-    base = eval_batch(sc, N2, Nu, d, l, refs)
-    assert not np.any(base.status & _lib.ST_NOT_RUN)
+    base = run_release("mixed")
+    assert not np.any(base["status"] & _lib.ST_NOT_RUN)
     # the general kernel's class launches in order: M <= 16 (k = 0), 32 (k = 1), 64 (k = 2); launch 0
     # also writes the padding / bad-horizon statuses
     for k, (lo, hi) in ((1, (16, 32)), (2, (32, 64))):
-        monkeypatch.setenv("MPCT_DIAG_DROP_LAUNCH", str(k))
-        res = eval_batch(sc, N2, Nu, d, l, refs)
-        monkeypatch.delenv("MPCT_DIAG_DROP_LAUNCH")
+        res = run_diag("mixed", tmp_path, MPCT_DIAG_DROP_LAUNCH=k)
         dropped = valid & (M > lo) & (M <= hi)
         assert dropped.sum() > 10
-        st = res.status.reshape(N2.size, -1)
+        st = res["status"].reshape(N2.size, -1)
         assert np.all(st[dropped] == _lib.ST_NOT_RUN), np.unique(st[dropped])
         assert np.all(failed(st[dropped]))
-        J1 = res.J1.reshape(N2.size, -1, 3)
+        J1 = res["J1"].reshape(N2.size, -1, 3)
         assert np.all(np.isnan(J1[dropped]))
-        assert np.all(res.qp_iters.reshape(N2.size, -1)[dropped] == 0)
+        assert np.all(res["qp_iters"].reshape(N2.size, -1)[dropped] == 0)
         keep = ~dropped
-        np.testing.assert_array_equal(st[keep], base.status.reshape(N2.size, -1)[keep])
-        np.testing.assert_array_equal(J1[keep], base.J1.reshape(N2.size, -1, 3)[keep])
+        np.testing.assert_array_equal(st[keep], base["status"].reshape(N2.size, -1)[keep])
+        np.testing.assert_array_equal(J1[keep], base["J1"].reshape(N2.size, -1, 3)[keep])

@@ -33,7 +33,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "dia
 from section_isa import VALU, section_counts  # noqa: E402
 
 SECTIONS = ["prologue", "plant", "y_update", "unconstrained", "qp(rest)", "u_update", "open_loop",
-            "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations"]
+            "qp.check", "qp.d+z", "qp.r+t1", "qp.add", "qp.drop", "qp.warm", "qp.rotations",
+            "qp.w.entry", "qp.w.rebuild", "qp.w.gather", "qp.w.solve", "qp.w.drop", "qp.w.rotations", "qp.w.readds"]
 
 # The chain of each section, per execution, as primitive -> count.  Read off gpc_small.hip's step
 # loop and gpc_qp16.h (file:line in the comments); names are tools/latency_probe.hip's probes.
@@ -66,19 +67,35 @@ CHAINS = {
     # two entries read, rsq, the RMW of R_A and B, lds_sync), B's row shift (gpc_qp16.h:268-322);
     # priced per drop with one rotation (the counted rotations add per rotation below)
     "qp.drop": {"bcast_readlane": 1, "lds_handoff": 3, "dpp_stage_f64": 1},
-    # warm start: the slacks' gather by ds_bpermute, w = B'c (row16 DPP), x = x_u + J w and
-    # lambda = B w (FOR4 chains + permlane row4 sums), the multipliers' exact argmin, the
-    # branch (gpc_qp16.h:396-440); per pass of its loop
+    # warm start (round 6: five stamps instead of one).  Pre-r06 dumps price the
+    # whole warm start as one pass of its solve loop per QP (the first model, 14.7x below measured)
     "qp.warm": {"shfl_bpermute": 1, "mul_f64": 1, "row_sum16": 1, "fma_f64": 4, "row4_sum_permlane": 1,
                 "add_f64": 1, "qargmin16_exact": 1, "uniform_branch": 1},
+    # the entry test of an infeasible x_u: box slacks, their min, the ballot (gpc_qp16.h gi_qp16 entry)
+    "qp.w.entry": {"block_prefix16_nu5": 1, "add_f64": 4, "ballot_branch": 1},
+    # the slacks' gather of c = b_A - N_A'x_u by ds_bpermute after the hand-off of the rebuild
+    "qp.w.gather": {"lds_handoff": 1, "shfl_bpermute": 1},
+    # one pass of the equality solve: B's row (LDS read), w = B'c (row16 DPP), x = x_u + J w and
+    # lambda = B w (FOR4 chains + permlane row4 sums), the multipliers' exact argmin
+    "qp.w.solve": {"lds_read_chase": 1, "mul_f64": 1, "row_sum16": 1, "fma_f64": 4, "row4_sum_permlane": 1,
+                   "add_f64": 1, "qargmin16_exact": 1},
+    # one warm drop: the branch into it, the drop (as qp.drop), c's lane shift; its rotations below
+    "qp.w.drop": {"uniform_branch": 1, "bcast_readlane": 1, "lds_handoff": 3, "dpp_stage_f64": 2},
+    # the rebuild: J <- R^-1 (one hand-off); per re-add below
+    "qp.w.rebuild": {"lds_handoff": 1},
 }
+# one re-add of the rebuild: the hand-off, B's row, d = J'n_p, the products, the add
+READD = {"lds_handoff": 2, "row_sum16": 1, "mul_f64": 2, "add_f64": 4, "row4_sum_permlane": 1,
+         "bcast_readlane": 1, "rsq_nr": 1, "fma_f64": 2, "rcp_nr": 1}
 # one Givens rotation of the drop: entries read, a^2 + b^2, rsq + Newton, cs / sn, the RMW of R_A's
 # two rows, lds_sync (gpc_qp16.h:289-310)
 ROTATION = {"lds_handoff": 1, "fma_f64": 1, "rsq_nr": 1, "mul_f64": 1}
 # the profile build's stamp closing each section (section_isa.py names; #1: the QP loop's check)
 ISA_SECTION = {"plant": "PROF_PLANT #0", "y_update": "PROF_YUPD #0", "unconstrained": "PROF_UNC #0",
                "u_update": "PROF_UUPD #0", "qp.check": "PROF_QCHECK #1", "qp.d+z": "PROF_QD #0",
-               "qp.r+t1": "PROF_QR #0", "qp.add": "PROF_QADD #0", "qp.drop": "PROF_QDROP #0"}
+               "qp.r+t1": "PROF_QR #0", "qp.add": "PROF_QADD #0", "qp.drop": "PROF_QDROP #0",
+               "qp.w.entry": "PROF_QWENTRY #0", "qp.w.gather": "PROF_QWGATH #0", "qp.w.solve": "PROF_QWSOLVE #0",
+               "qp.w.drop": "PROF_QWDROP #0"}
 STAMP_VALU = 6  # ProfAcc.add: lane id copy, compare, two selects, 64-bit add (wave_ops.h)
 
 
@@ -99,14 +116,16 @@ def main():
             valu.setdefault(closer, sum(row.get(c, 0) for c in VALU) - STAMP_VALU)
     lat = json.load(open(a.probe))
     raw = np.fromfile(a.prof, dtype=np.uint64)
-    width = len(SECTIONS) if raw.size % len(SECTIONS) == 0 and raw.size % 13 else 13  # pre-r05 dumps: 13
+    # r06 dumps: 21 words per simulation; r05: 14 (no warm-start split); before: 13
+    width = next(w for w in (len(SECTIONS), 14, 13) if raw.size % w == 0)
     raw = raw.reshape(-1, width)
-    cyc = (raw & np.uint64((1 << 48) - 1)).astype(np.float64)
-    cnt = (raw >> np.uint64(48)).astype(np.float64)
+    shift = 40 if width > 14 else 48  # count field: 24 bits since r06 (wave_ops.h kProfCountShift)
+    cyc = (raw & np.uint64((1 << shift) - 1)).astype(np.float64)
+    cnt = (raw >> np.uint64(shift)).astype(np.float64)
     S = raw.shape[0]
     rows = {}
     model = measured = bound = 0.0
-    for k, name in enumerate(SECTIONS):
+    for k, name in enumerate(SECTIONS[:width]):
         if name not in CHAINS:
             continue
         per = chain_cycles(CHAINS[name], lat)
@@ -117,6 +136,12 @@ def main():
         mod = per * n
         if name == "qp.drop" and width > 13:  # plus the counted Givens rotations of every drop
             mod += chain_cycles(ROTATION, lat) * cnt[:, SECTIONS.index("qp.rotations")].mean()
+        if name == "qp.w.drop":  # the warm drops' rotations
+            mod += chain_cycles(ROTATION, lat) * cnt[:, SECTIONS.index("qp.w.rotations")].mean()
+        if name == "qp.w.rebuild":  # its re-adds
+            mod += chain_cycles(READD, lat) * cnt[:, SECTIONS.index("qp.w.readds")].mean()
+        if name == "qp.warm" and width > 14:  # split into the qp.w.* sections: the rest is a stamp
+            per, mod = 0.0, 0.0
         rows[name] = dict(executions=round(n, 1), chain_cycles=round(per, 1), model=round(mod),
                           measured=round(m), frac=round(mod / m, 3) if m else None)
         b = mod
