@@ -32,6 +32,7 @@ __device__ __forceinline__ CInfo cinfo(int p, int Nu) {
 struct RowCons {
   double dmin, dmax, umin, umax;
   int n, l;
+  const double* bnd;  // (gi_qp16<.., true>) the row's MV bounds dmin, dmax, umin, umax in LDS instead
 };
 
 // Goldfarb-Idnani dual active-set QP (Goldfarb & Idnani 1983; the toolbox's KWIK is of this

@@ -50,9 +50,7 @@ struct RegFactors {
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
 // candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
 constexpr int kBS = 16;
-#ifndef MPCT_DROP_MERGE
-#define MPCT_DROP_MERGE 0
-#endif
+
 // Drops keep R_A and its Givens chain: drops derived from B alone, as the band kernel's (DESIGN §11
 // round 5), measured the same at 4096 candidates and 1 % slower on the heaviest 256 here (DESIGN §6
 // round 5): the metric's drops average three rotations, and J's register rotations dominate them.
@@ -60,7 +58,9 @@ constexpr int kBS = 16;
 // (all loads, then all stores) and the Givens chain with R_A's row and B's column carried in
 // registers, (a, c) by readlane and no hand-off per rotation, were 3-12 % slower at 4096 candidates
 // and on the heaviest 256: both add live values to a step loop at the 128-VGPR budget, whose
-// allocator answers with 2-5 more step-loop invariants spilled and reloaded every step
+// allocator answers with 2-5 more step-loop invariants spilled and reloaded every step.  The same
+// R_A(jj, jj) by readlane alone (loaded one rotation ahead otherwise) was 1-4 % slower as well,
+// with or without the bounds in LDS (profiles/r06c_metric_ab.txt)
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
@@ -293,21 +293,16 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
   const int idk = __builtin_amdgcn_readlane(S.ww, kd);
   mark(S, idk, false);
   lds_sync();  // R_A and B columns written by the adds
-#if MPCT_DROP_MERGE
   // R_A loses column kd (lanes = rows) and B loses row kd (lanes = columns) in one loop, before the
   // rotations: removing a row of B commutes with rotating its columns (B G' minus row kd), so the
-  // two serial shift chains run side by side instead of one after the other
+  // two serial shift chains run side by side instead of one after the other (round 6: 0.5 % on the
+  // metric alone, 1.7 % with the bounds in LDS; bitwise the same; profiles/r06c_metric_ab.txt)
   if (lane < q) {
     for (int w = kd; w < q - 1; ++w) {
       sRA[lane * M + w] = sRA[lane * M + w + 1];
       sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
     }
   }
-#else
-  if (lane < q) {  // remove column kd (lanes = rows of row block 0)
-    for (int w = kd; w < q - 1; ++w) sRA[lane * M + w] = sRA[lane * M + w + 1];
-  }
-#endif
   {
     const double un = lane_next<16>(S.uw);
     const int wn = lane_next_i<16>(S.ww);
@@ -329,7 +324,7 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
         sRA[jj * M + lane] = cs * r0 + sn * r1;
         sRA[(jj + 1) * M + lane] = (lane == jj) ? 0.0 : -sn * r0 + cs * r1;
       }
-      if (lane < q) {  // B G': columns jj, jj + 1 (lanes = rows)
+      if (lane < q) {  // B G': columns jj, jj + 1 (lanes = rows; row q - 1 is stale after the shift, unused)
         const double b0 = sB[lane * kBS + jj], b1 = sB[lane * kBS + jj + 1];
         sB[lane * kBS + jj] = cs * b0 + sn * b1;
         sB[lane * kBS + jj + 1] = -sn * b0 + cs * b1;
@@ -339,12 +334,6 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
     }
     lds_sync();
   }
-#if !MPCT_DROP_MERGE
-  // row kd of B G' leaves (lanes = columns)
-  if (lane < q - 1) {
-    for (int w = kd; w < q - 1; ++w) sB[w * kBS + lane] = sB[(w + 1) * kBS + lane];
-  }
-#endif
   const int qn = q - 1;
   if (i == qn) {
     S.uw = 0.0;
@@ -358,7 +347,7 @@ __device__ __forceinline__ void gi16_drop(GIState<16>& S, RegFactors& F, double*
 // up_row, the row's constraint data rc (both replicated over the four row blocks); the optimal
 // moves come back in xout (row vector, registers; xu itself when it is feasible).  rebuild: the
 // J rebuild interval in units of M rotations (gpc_qp.h); PACKED: R^-1's layout (rinv_idx)
-template <bool PACKED = false, class PAcc = void>
+template <bool PACKED = false, class PAcc = void, bool BLDS = false>
 __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, int Nu,
                                        const RowCons& rc, double up_row, double xu, double tol, int maxit,
                                        int* st, GIState<16>& S, RegFactors& F, int rebuild, double& xout
@@ -370,19 +359,44 @@ __device__ __forceinline__ int gi_qp16(const double* sRi, double* sRA, int M, in
   const bool row = i < M;
   if (!row) up_row = 0.0;
   const int rl = rc.l;
-  const double lo_box = fmax(rc.dmin, rc.umin - up_row), hi_box = fmin(rc.dmax, rc.umax - up_row);
+  // BLDS (gpc_small_kernel): the row's bounds are read from LDS where a check needs them (the two
+  // 16-byte loads issue under the block prefix's DPP chain) instead of living in eight VGPRs
+  // across the whole step loop: the kernel's last VGPR spills go (2 -> 0, no scratch), and with
+  // the merged drop shifts the metric is 1.7 % faster (profiles/r06c_metric_ab.txt)
+  double lo_box = 0.0, hi_box = 0.0;
+  if constexpr (!BLDS) {
+    lo_box = fmax(rc.dmin, rc.umin - up_row);
+    hi_box = fmin(rc.dmax, rc.umax - up_row);
+  }
   auto slacks = [&](double x, double s[4]) {
+    double dmin, dmax, umin, umax, lo, hi;
+    if constexpr (BLDS) {
+      const double2 a = reinterpret_cast<const double2*>(rc.bnd)[0], b = reinterpret_cast<const double2*>(rc.bnd)[1];
+      dmin = a.x;
+      dmax = a.y;
+      umin = b.x;
+      umax = b.y;
+      lo = fmax(dmin, umin - up_row);
+      hi = fmin(dmax, umax - up_row);
+    } else {
+      dmin = rc.dmin;
+      dmax = rc.dmax;
+      umin = rc.umin;
+      umax = rc.umax;
+      lo = lo_box;
+      hi = hi_box;
+    }
     const double pre = block_prefix<16>(x, rl, Nu, row, nullptr);
     if (rl == 0) {
-      s[0] = x - lo_box;
-      s[1] = hi_box - x;
+      s[0] = x - lo;
+      s[1] = hi - x;
       s[2] = INFINITY;
       s[3] = INFINITY;
     } else {
-      s[0] = x - rc.dmin;
-      s[1] = rc.dmax - x;
-      s[2] = pre - (rc.umin - up_row);
-      s[3] = (rc.umax - up_row) - pre;
+      s[0] = x - dmin;
+      s[1] = dmax - x;
+      s[2] = pre - (umin - up_row);
+      s[3] = (umax - up_row) - pre;
     }
     if (!row) s[0] = s[1] = s[2] = s[3] = INFINITY;
   };

@@ -41,9 +41,9 @@
 namespace mpct {
 
 // LDS layout of one simulation (doubles, 16-byte aligned pieces)
-// (the Shell 3x3 metric, M = 15: 10,064 B, so 16 workgroups fit a CU's 160 KB)
+// (the Shell 3x3 metric, M = 15: 10,160 B, so 16 workgroups fit a CU's 160 KB)
 struct SmallLayout {
-  int rinv, ra, gb, A, xy, ring, hist, total;
+  int rinv, ra, gb, A, xy, ring, hist, bnd, total;
 };
 __host__ __device__ inline SmallLayout small_layout(const DevScenario& sc, int M) {
   SmallLayout L;
@@ -56,6 +56,7 @@ __host__ __device__ inline SmallLayout small_layout(const DevScenario& sc, int M
   L.xy = take(kSmY);                // y part of x
   L.ring = take(3 * 2 * kSmR);      // past-control rings, two copies each
   L.hist = take(kSmEOff + 4 * sc.my * sc.sm_ke);  // input rings [3][kSmU] | entry output rings [4 my][ke]
+  L.bnd = take(4 * 3);                            // MV bounds [nu][dmin, dmax, umin, umax] (96 B)
   L.total = (o + 1) & ~1;
   return L;
 }
@@ -68,7 +69,7 @@ __device__ __forceinline__ int sm_lane() {
   return l;
 }
 
-// four waves per SIMD: 128 VGPRs (one plant coefficient spilled and re-read per step) and 10 KB of
+// four waves per SIMD: 128 VGPRs (no spill since round 6: the QP rows' bounds live in LDS) and 10 KB of
 // LDS, so 16 workgroups fit a CU and the metric's 4096 simulations run in one round.  Against three
 // waves: bitwise the same results, 3.11-3.19 against 3.38-3.46 ms at 8192 candidates, the same
 // 2.21-2.24 ms at 4096 (profiles/r04b_small_ab.txt)
@@ -104,6 +105,9 @@ __global__ void __launch_bounds__(64, 4)
 #ifdef MPCT_PROFILE
   ProfAcc pacc;
   unsigned long long pprev = __builtin_amdgcn_s_memtime();
+  using PAccT = ProfAcc;
+#else
+  using PAccT = void;
 #endif
   const SmallLayout L = small_layout(sc, M);
   double* sA = lds + L.A;
@@ -120,9 +124,9 @@ __global__ void __launch_bounds__(64, 4)
 
   // per-lane constants of the step loop
   // plant term: coefficient, ring (LDS double index), delay, ring mask
-  // the plant coefficient lives across the loop; the 128-VGPR budget spills it and reloads it
-  // from scratch at the top of every step.  Re-reading it from the scenario table under the
-  // u update instead (no spill) measured 2.5 % slower on the heaviest 256
+  // the plant coefficient lives across the loop (round 5 spilled it to scratch and reloaded it at
+  // the top of every step; re-reading it from the scenario table instead measured 2.5 % slower on
+  // the heaviest 256; the bounds in LDS freed the registers in round 6)
   const double pcoef = sc.sm_coef[lane];
   const int pbase = L.hist + sc.sm_hoff[lane];
   const int pc = sc.sm_hc[lane], pmask = sc.sm_hmask[lane];
@@ -139,10 +143,9 @@ __global__ void __launch_bounds__(64, 4)
   RowCons rcn;
   rcn.n = qm < M ? qm / Nu : 0;
   rcn.l = qm < M ? qm - rcn.n * Nu : 0;
-  rcn.dmin = sc.bnd[rcn.n];
-  rcn.dmax = sc.bnd[nu + rcn.n];
-  rcn.umin = sc.bnd[2 * nu + rcn.n];
-  rcn.umax = sc.bnd[3 * nu + rcn.n];
+  // the row's MV bounds stay in LDS (gpc_qp16.h BLDS), stored before the loop's first lds_sync
+  if (lane < 4 * nu) lds[L.bnd + lane] = sc.bnd[(lane & 3) * nu + (lane >> 2)];
+  rcn.bnd = lds + L.bnd + 4 * rcn.n;
   const double tol = o.feas_tol;
   const int maxit = o.max_qp_iter > 0 ? o.max_qp_iter : 8 * M + 16;
   const int ink0 = sc.ink0;
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(64, 4)
     // ---- QP (gpc_qp16.h): u(t-1) of the row's MV from lane n
     double xq;
     const double up_row = __shfl(uprev, rcn.n, kWave);
-    iters += gi_qp16<true>(lds + L.rinv, lds + L.ra, M, Nu, rcn, up_row, xu, tol, maxit, &st, gis, rf,
+    iters += gi_qp16<true, PAccT, true>(lds + L.rinv, lds + L.ra, M, Nu, rcn, up_row, xu, tol, maxit, &st, gis, rf,
                      kGiRebuild16, xq
 #ifdef MPCT_PROFILE
                      , pacc, pprev

@@ -1,8 +1,12 @@
 #!/bin/bash
-# r06b: the QP-cap fault tests again (band batch: no clean simulation), the config-3 LPT plan sweep
-# from the committed cell table, and the metric's heaviest-256 profile with the warm start split
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06b}; O="gpurun_out/$T"; mkdir -p "$O"
-bash tools/gpu_steps.sh "$O" \
-  "300 pytest python3 -u -m pytest tests/test_qp_caps.py tests/test_not_run.py -m gpu -x -v --timeout 240 --timeout-method thread" \
-  "300 plans python3 tools/shard_balance.py --only shell7x5 --plans 1:none,0.4:none,0.3:none,0.5:none,0.4:100,0.4:80 --out $O/shard_plans.json" \
-  "120 kprof env MPCT_PROF_OUT=$O/prof_heavy256.bin python3 tools/kprof.py 256 heavy"
+# r06c: metric variants (bounds in LDS, merged drop shifts, R_A(jj,jj) by readlane) A/B, three
+# interleaved rounds with bitwise dumps; config-3 plans at the fitted overlap
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06c}; O="gpurun_out/$T"; mkdir -p "$O"
+AB=()
+for rep in 1 2 3; do
+  for v in base mrg bnd bm bma ma; do
+    AB+=("45 ab_${v}_$rep env MPCT_LIB=$R/model-predictive-control-tuning_amd/csrc/libmpct_$v.so QAB_DUMP=$O/ab_$v.npz python3 tools/qab.py h256 4096 8192")
+  done
+done
+bash tools/gpu_steps.sh "$O" "${AB[@]}" \
+  "200 plans python3 tools/shard_balance.py --only shell7x5 --plans 0.54:none,0.5:none --out $O/shard_plans.json"
