@@ -552,11 +552,16 @@ long long small_lds_bytes(const DevScenario& sc, int M);  // gpc_small.hip
 int launch_small(const DevScenario& sc, long long C, int nref, const int* N2, const int* Nu, const double* delta,
                  const double* lambda, const double* r, const DevOpts& o, const DevResult& out, const int* perm,
                  int first, hipStream_t stream, std::string* err);
+long long dtc_small_lds_bytes(const DevScenario& sc, int M);  // dtc_small.hip
+int launch_dtc_small(const DevScenario& sc, int cls, long long C, int nref, const int* N2, const int* Nu,
+                     const double* delta, const double* lambda, const double* r, const double* v, const DevOpts& o,
+                     const DevResult& out, const int* perm, int mlo, int first, hipStream_t stream, std::string* err);
 
 long long lds_bytes_for(const DevScenario& sc, int N2, int Nu, bool ext) {
   (void)N2;
   const int M = sc.nu * Nu;
   if (sc.small && !ext && M <= 16) return small_lds_bytes(sc, M);
+  if (sc.small_dtc && !ext && M <= 32) return dtc_small_lds_bytes(sc, M);
   LdsLayout L = lds_layout(sc, M, ext);
   return (long long)L.total * 8;
 }
@@ -610,8 +615,13 @@ std::string closed_loop_instance(const DevScenario& sc, int maxM, bool ext) {
       nm = "gpc_small_kernel";
       continue;
     }
+    if (cls <= 32 && sc.small_dtc && !ext) {
+      nm += (nm.empty() ? "" : " + ") + std::string("dtc_small_kernel<") + std::to_string(cls) + ">";
+      continue;
+    }
     if (nm.empty()) nm = "gpc_closed_loop_kernel<" + std::to_string(cls) + tail;
-    else if (nm == "gpc_small_kernel") nm += " + gpc_closed_loop_kernel<" + std::to_string(cls) + tail;
+    else if (nm.find("gpc_closed_loop_kernel") == std::string::npos)
+      nm += " + gpc_closed_loop_kernel<" + std::to_string(cls) + tail;
     else nm += " + <" + std::to_string(cls) + tail;
   }
   return nm;
@@ -659,6 +669,8 @@ int launch_closed_loop(const DevScenario& sc, long long C, int nref, const int* 
     const bool ext = o.open_loop || o.want_traj;
     if (diag_drop_launch(k)) rc = 0;
     else if (cls == 16 && sc.small && !ext) rc = launch_small(sc, C, nref, N2, Nu, delta, lambda, r, o, lo, perm, first, st, err);
+    else if (cls <= 32 && sc.small_dtc && !ext)
+      rc = launch_dtc_small(sc, cls, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else if (cls == 16) rc = launch_t<16>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else if (cls == 32) rc = launch_t<32>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);
     else rc = launch_t<64>(sc, C, nref, N2, Nu, delta, lambda, r, v, o, lo, perm, mlo, first, st, err);

@@ -22,7 +22,9 @@ namespace mpct {
 // upper triangle row by row, gpc_qp16.h rinv_idx) in sRi; the gain
 // A = -R^-1 T with state column vc of row m at sA[m * astride + acol(vc)] (acol: host column map,
 // nullptr = identity).  Returns false (uniformly) when R is not positive definite.
-template <int MAXM, bool PACKED = false>
+// RINV = false: no R^-1 (an unconstrained loop has no QP); FIRST = true: only the first-move rows
+// m = n Nu of A, stored as row n (DTC_GPC_WW.m:105 Km: the unconstrained loop applies those alone)
+template <int MAXM, bool PACKED = false, bool RINV = true, bool FIRST = false>
 __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, int M, int Nu, int N2,
                                              const double* dl, const double* lm, double* sR, double* sRi,
                                              double* sA, int astride, const int* acol) {
@@ -147,14 +149,23 @@ __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, in
       }
       const int ac = acol ? acol[vc] : vc;
 #pragma unroll
-      for (int m = 0; m < MAXM; ++m)
-        if (m < M) sA[m * astride + ac] = -rcol[m];
+      for (int m = 0; m < MAXM; ++m) {
+        if constexpr (FIRST) {
+          if (m < M && m % Nu == 0) sA[(m / Nu) * astride + ac] = -rcol[m];
+        } else {
+          if (m < M) sA[m * astride + ac] = -rcol[m];
+        }
+      }
     }
   }
   // R^-1: lane j solves R x = e_j in its own LDS column (zeros below unless PACKED)
   auto ri = [&](int i, int k) __attribute__((always_inline)) -> int {
     return PACKED ? i * M - ((i * (i - 1)) >> 1) + (k - i) : i * M + k;
   };
+  if (!RINV) {
+    lds_sync();
+    return true;
+  }
   if (lane < M) {
     for (int kk = lane; kk >= 0; --kk) {
       double a = (kk == lane) ? 1.0 : 0.0;

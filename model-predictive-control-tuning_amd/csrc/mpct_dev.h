@@ -42,6 +42,7 @@ constexpr int kSmA = kSmY + 3 * kSmR;      // A row stride
 constexpr int kSmU = 16;                   // plant input ring per MV (power of two, > longest delay + taps)
 constexpr int kSmE = 4;                    // longest plant entry output ring (power of two > denominator taps)
 constexpr int kSmEOff = 3 * kSmU;          // entry output rings (4 my of them) after the input rings
+constexpr int kDtcEOff = 4 * kSmU;         // dtc_small_kernel: 4 input rings (MVs + plant-only disturbances)
 
 // per-simulation status bits (mirror of MPCT_ST_* in include/mpct.h)
 constexpr int MPCT_ST_QP_MAXITER_ = 1;
@@ -77,6 +78,10 @@ struct DevScenario {
   const int* sm_hc;       // [64]
   const int* sm_hmask;    // [64]
   const int* sm_acol;     // [nx]
+  // DTC-GPC small plants (dtc_small_kernel, dtc_small.hip; mpct_host.cpp dtc_small_plant): the sm_*
+  // lane tables are [nvar][64] (plant variant k % nvar) and the filters Fr_i [my][8] (fb 0..3, fa 0..3)
+  int small_dtc;
+  const double* sm_fr;
   // tables (device pointers into one allocation)
   const double* step;   // [my][nu][tlen]   model step responses s_ij(t), t = 0..tlen-1
   // dispatch-key Gram tables (work_order.hip order_keys_gpc; nullptr when not built): block

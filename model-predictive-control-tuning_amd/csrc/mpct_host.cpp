@@ -817,6 +817,88 @@ static bool small_plant(const mpct_scenario* s, SmallTables* tb = nullptr) {
   return true;
 }
 
+// dtc_small_kernel's lane tables (dtc_small.hip), or false when the scenario is not a DTC-GPC small
+// plant: DTC mode with every move bound infinite (DTC_GPC_WW.m's unconstrained loop: no QP), my <= 2,
+// nu <= 2, nu + nq <= 4 ring-fed inputs (no MDs), every entry of every plant variant, of Pz and of Gz
+// <= 4 terms with rings the kernel holds, filters of <= 4 taps, y difference state <= 4 per output,
+// past-control registers <= kSmR.  Tables: coef / hoff / hc / hmask [nvar][64] (lane L = 16 k + 4 q
+// + p: quads q < my the plant entries (i = q, input p), quads 2 + i: p < 2 Pz(i, p), p >= 2
+// Gz(i, p - 2)), the acol map as for gpc_small, filters fr [my][8] = fb 0..3 | fa 0..3
+static bool dtc_small_plant(const mpct_scenario* s, SmallTables* tb = nullptr, std::vector<double>* fr = nullptr) {
+  if (!s->dtc || s->mdband || s->nmpc || s->nd || s->my > 2 || s->nu > 2 || s->npin > 4) return false;
+  for (int n = 0; n < s->nu; ++n)
+    if (!(std::isinf(s->bnd[n]) && std::isinf(s->bnd[s->nu + n]) && std::isinf(s->bnd[2 * s->nu + n]) &&
+          std::isinf(s->bnd[3 * s->nu + n])))
+      return false;
+  if (s->nyh > kSmY) return false;
+  for (int i = 0; i < s->my; ++i)
+    if (s->nyhi[i] > 4 || s->fr_n[i] > 4) return false;
+  for (int n = 0; n < s->nu; ++n)
+    if (s->dum[n] > kSmR) return false;
+  int na_max = 0;
+  auto fits = [&](int nb, int off, int na) {
+    na_max = std::max(na_max, na - 1);
+    return (nb - off) + (na - 1) <= 4 && na - 1 < kSmE && nb <= kSmU;
+  };
+  for (int e = 0; e < s->nvar * s->ne; ++e)
+    if (!fits(s->pl_nb[e], s->pl_off[e], s->pl_na[e])) return false;
+  for (int e = 0; e < 2 * s->my * s->nu; ++e)
+    if (!fits(s->mz_nb[e], s->mz_off[e], s->mz_na[e])) return false;
+  if (!tb) return true;
+  tb->ke = na_max < 2 ? 2 : 4;
+  const int V = s->nvar;
+  tb->coef.assign((size_t)V * kWave, 0.0);
+  tb->hoff.assign((size_t)V * kWave, 0);
+  tb->hc.assign((size_t)V * kWave, 0);
+  tb->hmask.assign((size_t)V * kWave, kSmU - 1);
+  for (int v = 0; v < V; ++v)
+    for (int L = 0; L < kWave; ++L) {
+      const int k = L >> 4, ep = L & 15, q = ep >> 2, pp = ep & 3;
+      int nb, off, na, j;
+      const double *b, *a;
+      if (q < 2) {  // plant entry (q, pp) of variant v
+        if (q >= s->my || pp >= s->npin) continue;
+        const int e = v * s->ne + q * s->npin + pp;
+        nb = s->pl_nb[e], off = s->pl_off[e], na = s->pl_na[e], j = pp;
+        b = &s->pl_b[(size_t)e * s->pl_maxb];
+        a = &s->pl_a[(size_t)e * s->pl_maxa];
+      } else {  // Pz (pp < 2) / Gz (pp >= 2) entry (q - 2, pp & 1): the controller's own inputs
+        const int i = q - 2;
+        j = pp & 1;
+        if (i >= s->my || j >= s->nu) continue;
+        const int e = (pp >= 2 ? s->my * s->nu : 0) + i * s->nu + j;
+        nb = s->mz_nb[e], off = s->mz_off[e], na = s->mz_na[e];
+        b = &s->mz_b[(size_t)e * s->mz_maxb];
+        a = &s->mz_a[(size_t)e * s->mz_maxa];
+      }
+      const int nbz = nb - off, Li = v * kWave + L;
+      if (k < nbz) {  // b tap: input j at t - off - k
+        tb->coef[Li] = b[off + k];
+        tb->hoff[Li] = j * kSmU;
+        tb->hc[Li] = off + k;
+      } else if (k < nbz + na - 1) {  // a tap jj: -a_jj y_e(t - jj)
+        const int jj = k - nbz + 1;
+        tb->coef[Li] = -a[jj];
+        tb->hoff[Li] = kDtcEOff + ep * tb->ke;
+        tb->hc[Li] = jj;
+        tb->hmask[Li] = tb->ke - 1;
+      }
+    }
+  tb->acol.assign(s->nx, 0);
+  for (int c = 0; c < s->nyh; ++c) tb->acol[c] = c;
+  for (int n = 0; n < s->nu; ++n)
+    for (int k = 0; k < s->dum[n]; ++k) tb->acol[s->upoff[n] + k] = kSmY + kSmR * n + k;
+  if (fr) {
+    fr->assign((size_t)s->my * 8, 0.0);
+    for (int i = 0; i < s->my; ++i)
+      for (int l = 0; l < s->fr_n[i]; ++l) {
+        (*fr)[(size_t)i * 8 + l] = s->fr_b[(size_t)i * s->fr_max + l];
+        (*fr)[(size_t)i * 8 + 4 + l] = s->fr_a[(size_t)i * s->fr_max + l];
+      }
+  }
+  return true;
+}
+
 // longest run of numerator taps from each entry's first nonzero one (mdband_kernel.hip keeps only
 // those in LDS: the delay's leading zeros are skipped by pl_off / mz_off anyway)
 static void compact_taps(const mpct_scenario* s, DevScenario& ds) {
@@ -940,12 +1022,15 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   gram_tables(s, gram);
   size_t o_gram = put(gram.data(), gram.size() * 8);
   SmallTables smt;
+  std::vector<double> sfr;
   const bool small = small_plant(s, &smt);
+  const bool small_dtc = !small && dtc_small_plant(s, &smt, &sfr);
   size_t o_smc = put(smt.coef.data(), smt.coef.size() * 8);
   size_t o_smo = put(smt.hoff.data(), smt.hoff.size() * 4);
   size_t o_smh = put(smt.hc.data(), smt.hc.size() * 4);
   size_t o_smm = put(smt.hmask.data(), smt.hmask.size() * 4);
   size_t o_sma = put(smt.acol.data(), smt.acol.size() * 4);
+  size_t o_sfr = put(sfr.data(), sfr.size() * 8);
   void* dp = nullptr;
   if (hipMalloc(&dp, blob.size()) != hipSuccess) return fail(MPCT_ENOMEM, "hipMalloc(tables) failed");
   if (hipMemcpy(dp, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -984,6 +1069,8 @@ static int build_ctx(mpct_scenario* s, int dev, DevCtx** out) {
   ds.sm_hc = reinterpret_cast<const int*>(b + o_smh);
   ds.sm_hmask = reinterpret_cast<const int*>(b + o_smm);
   ds.sm_acol = reinterpret_cast<const int*>(b + o_sma);
+  ds.small_dtc = small_dtc ? 1 : 0;
+  ds.sm_fr = reinterpret_cast<const double*>(b + o_sfr);
   ds.step = reinterpret_cast<const double*>(b + o_step);
   ds.gram = gram.empty() ? nullptr : reinterpret_cast<const double*>(b + o_gram);
   ds.phi = reinterpret_cast<const double*>(b + o_phi);
@@ -1427,6 +1514,7 @@ extern "C" int32_t mpct_kernel_instance(const mpct_scenario* s, const mpct_opts*
     ds.dtc = s->dtc;
     ds.regpath = regpath(s);
     ds.small = small_plant(s) ? 1 : 0;
+    ds.small_dtc = !ds.small && dtc_small_plant(s) ? 1 : 0;
     nm = closed_loop_instance(ds, s->nu * s->numax, ext);
   }
   if (buf && cap > 0) {
@@ -1458,6 +1546,7 @@ static int64_t lds_bytes_ext(const mpct_scenario* s, int32_t N2, int32_t Nu, boo
   {
     SmallTables smt;
     ds.small = small_plant(s, &smt) ? 1 : 0;
+    ds.small_dtc = !ds.small && dtc_small_plant(s, &smt) ? 1 : 0;
     ds.sm_ke = smt.ke;
   }
   ds.my = s->my;

@@ -274,6 +274,23 @@ def test_kernel_instance_and_multi_validation(built):
         eval_batch_multi(sc, [], N2, 5, d, d, r[None])
     lib = _lib.load()
     assert lib.mpct_kernel_instance(None, None, None, 0) < 0
+    # DTC mode (DTC_GPC_WW.m): unconstrained -> dtc_small_kernel for cost-only batches (both QP-size
+    # classes), the general DTC instances with trajectories or with any finite move bound
+    from mpct.dtc import woodberry_dtc, woodberry_mc
+
+    scm, _, _, _ = woodberry_mc(draws=4, n2_max=30, nu_max=10)
+    assert kernel_instance(scm) == "dtc_small_kernel<16> + dtc_small_kernel<32>"
+    assert kernel_instance(scm, want_traj=True) == "gpc_closed_loop_kernel<16,true,true> + <32,true,true>"
+    scd, _, _ = woodberry_dtc(n2_max=10, nu_max=5)
+    assert kernel_instance(scd) == "dtc_small_kernel<16>"
+    from mpct.engine import Scenario
+
+    b = np.array([0.5, 0.5])
+    scb = Scenario(scd.plant, scd.model, nu=2, du_min=-b, du_max=b, u_min=-np.full(2, np.inf),
+                   u_max=np.full(2, np.inf), yref=np.zeros((2, 200)), n2_max=10, nu_max=5, Ts=1.0, window="gpc",
+                   weights_squared=False, exact_carima=False, dtc=True, dist=[[t] for t in (scd.plant[0][0],
+                                                                                           scd.plant[1][0])])
+    assert kernel_instance(scb) == "gpc_closed_loop_kernel<16,true,false>"
 
 
 def test_library_derived_carima_equals_host(built):

@@ -155,9 +155,32 @@ def test_dtc_monte_carlo_variants(gpu):
     d = 10.0 ** rng.uniform(-1, 1, (C, 2))
     l = 10.0 ** rng.uniform(-1, 1, (C, 2))
     res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
-    _oracle_compare(res, C, D, N2, Nu, d, l, [(c, k) for c in range(C) for k in (0, 2, 3)], plants)
+    pairs = [(c, k) for c in range(C) for k in (0, 2, 3)]
+    _oracle_compare(res, C, D, N2, Nu, d, l, pairs, plants)
     mean, worst = robust_scores(res.J1, C, D)
     assert np.all(worst >= mean)
+    # the cost-only batch runs dtc_small_kernel (no QP: the loop is unconstrained): its J1 against
+    # the same reference-structured loop, draw by draw
+    cost = eval_batch(sc, N2, Nu, d, l, refs, v=v)
+    _oracle_costs(cost, D, N2, Nu, d, l, pairs, plants)
+
+
+def _oracle_costs(res, D, N2, Nu, d, l, pairs, plants):
+    """J1 of simulations (c, k) of a cost-only batch against DTC_GPC_WW.m's loop on draw k's plant,
+    1e-6 relative (the BASELINE tolerance); non-finite on both sides where the draw diverges."""
+    from oracle.dtcgpc import dtc_gpc_ww
+
+    for c, k in pairs:
+        s = c * D + k
+        p, m = int(N2[c]), int(Nu[c])
+        ref = dtc_gpc_ww(p=(p, p), m=(m, m), lam=tuple(l[c]), delta=tuple(d[c]), plant=plants[k])
+        J1 = np.sum((ref["y"] - ref["r"]) ** 2, axis=1)
+        if not np.all(np.isfinite(J1)):
+            assert res.status[s] & 4, (c, k, res.status[s])
+            continue
+        assert res.status[s] == 0, (c, k, res.status[s])
+        ej = float(np.max(np.abs(res.J1[s] - J1) / np.abs(J1)))
+        assert ej < 1e-6, (c, k, p, m, ej)
 
 
 @pytest.mark.gpu
@@ -179,16 +202,40 @@ def test_config4_range_against_oracle(gpu):
     from mpct.engine import kernel_instance
 
     assert kernel_instance(sc, want_traj=True) == "gpc_closed_loop_kernel<16,true,true> + <32,true,true>"
-    assert kernel_instance(sc) == "gpc_closed_loop_kernel<16,true,false> + <32,true,false>"
+    assert kernel_instance(sc) == "dtc_small_kernel<16> + dtc_small_kernel<32>"
     res = eval_batch(sc, N2, Nu, d, l, refs, v=v, want_traj=True)
     cost = eval_batch(sc, N2, Nu, d, l, refs, v=v)   # the cost-only instance the bench times
     ok = res.status == 0
+    # two kernels (the general one with trajectories, dtc_small_kernel for costs): the same loop
+    # with the plant terms summed in another order, so equal to rounding, not bitwise
     np.testing.assert_array_equal(cost.status, res.status)
-    np.testing.assert_allclose(cost.J1[ok], res.J1[ok], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(cost.J1[ok], res.J1[ok], rtol=1e-9, atol=0)
     plants = woodberry_mc_draws(D)
     pairs = [(c, (5 * c + j * 11) % D) for c in range(len(idx)) for j in range(3)]
     worst = _oracle_compare(res, len(idx), D, N2, Nu, d, l, pairs, plants)
+    _oracle_costs(cost, D, N2, Nu, d, l, pairs, plants)
     print("config-4 range: %d pairs, max traj rel err %.2e" % (len(pairs), worst))
+
+
+@pytest.mark.gpu
+def test_dtc_small_kernel_against_general(gpu):
+    """dtc_small_kernel (cost-only, the config-4 bench's launch) against the general DTC kernel
+    (the trajectory instance) over every draw of 96 seeded config-4 candidates spanning both QP-size
+    classes: identical statuses, J1 and j22 equal to 1e-9 relative wherever the loop stays finite."""
+    from mpct.dtc import config4_candidates, woodberry_mc
+    from mpct.engine import eval_batch
+
+    D = 32
+    sc, refs, v, _ = woodberry_mc(draws=D, n2_max=30, nu_max=10)
+    N2, Nu, d, l = config4_candidates(10000)
+    idx = np.concatenate([np.arange(64), np.flatnonzero(2 * Nu > 16)[:32]])
+    cost = eval_batch(sc, N2[idx], Nu[idx], d[idx], l[idx], refs, v=v)
+    gen = eval_batch(sc, N2[idx], Nu[idx], d[idx], l[idx], refs, v=v, want_traj=True)
+    np.testing.assert_array_equal(cost.status, gen.status)
+    ok = cost.status == 0
+    assert ok.mean() > 0.5 and np.all(cost.qp_iters == 0)
+    np.testing.assert_allclose(cost.J1[ok], gen.J1[ok], rtol=1e-9, atol=0)
+    np.testing.assert_allclose(cost.j22[ok], gen.j22[ok], rtol=1e-9, atol=0)
 
 
 @pytest.mark.gpu

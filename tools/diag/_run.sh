@@ -1,12 +1,14 @@
 #!/bin/bash
-# r06c: metric variants (bounds in LDS, merged drop shifts, R_A(jj,jj) by readlane) A/B, three
-# interleaved rounds with bitwise dumps; config-3 plans at the fitted overlap
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06c}; O="gpurun_out/$T"; mkdir -p "$O"
+# r06d: the GPU suite with dtc_small_kernel (config 4's cost-only launches), the dtc-mc bench line
+# for three occupancy variants of that kernel, interleaved, and the metric bench line
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06d}; O="gpurun_out/$T"; mkdir -p "$O"
 AB=()
-for rep in 1 2 3; do
-  for v in base mrg bnd bm bma ma; do
-    AB+=("45 ab_${v}_$rep env MPCT_LIB=$R/model-predictive-control-tuning_amd/csrc/libmpct_$v.so QAB_DUMP=$O/ab_$v.npz python3 tools/qab.py h256 4096 8192")
+for rep in 1 2; do
+  for v in dw1 dw5 dw6; do
+    AB+=("90 dtc_${v}_$rep env MPCT_LIB=$R/model-predictive-control-tuning_amd/csrc/libmpct_$v.so python3 bench.py --workload dtc-mc --no-cpu-baseline")
   done
 done
-bash tools/gpu_steps.sh "$O" "${AB[@]}" \
-  "200 plans python3 tools/shard_balance.py --only shell7x5 --plans 0.54:none,0.5:none --out $O/shard_plans.json"
+bash tools/gpu_steps.sh "$O" \
+  "420 pytest python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread" \
+  "${AB[@]}" \
+  "200 bench python3 bench.py --no-cpu-baseline"

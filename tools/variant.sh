@@ -6,7 +6,7 @@ set -e
 C=/root/repo/model-predictive-control-tuning_amd/csrc; NAME=$1; shift
 K=${K:-gpc_kernel.hip}
 OBJS=""
-for u in gpc_kernel gpc_small mdband_kernel nmpc_kernel work_order; do
+for u in gpc_kernel gpc_small dtc_small mdband_kernel nmpc_kernel work_order; do
   if [ "$u.hip" = "$K" ] || { [ "$K" = all ] && [ $u != work_order ]; }; then
     UF=""; [ $u = gpc_small ] && UF="-mllvm -amdgpu-sched-strategy=max-ilp -mllvm -misched-prera-direction=topdown"  # __graft_entry__.UNIT_FLAGS
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $UF "$@" -c $C/$u.hip -o /tmp/${u}_$NAME.o
