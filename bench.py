@@ -69,6 +69,26 @@ def nmpc_flops_per_sim(N, Nu, gn_iters, nit=60, nsub=10, nx=3, ny=2, nu=2):
     return gn_iters * per_gn + nit * nsub * 4 * 40
 
 
+def dtc_flops_per_sim(sc, N2, Nu):
+    """Algorithmic flops of one config-4 simulation as dtc_small_kernel computes it (the
+    unconstrained DTC loop applies only the first-move rows of the gain): setup P*M*(M+1) + M^3/3
+    (SURVEY §8d's term); per step 2 flops per term of every plant / disturbance-path entry and of
+    every predictor entry Pz, Gz (nonzero numerator taps + denominator order), the filters
+    2*(2*len - 1) per output, the y difference update 4 per output, the first-move product
+    2*nu*nx, the costs 4*my."""
+    def terms(t):
+        return int(np.count_nonzero(np.asarray(t.num))) + len(t.den) - 1
+
+    my, nu = sc.my, sc.nu
+    nx = int(sc.table(2)[6])
+    plant = sum(terms(t) for row in sc.plant for t in row) + sum(terms(t) for row in (sc.dist or []) for t in row)
+    model = 2 * sum(terms(t) for row in sc.model for t in row[:nu])
+    filt = sum(2 * (2 * len(f.den) - 1) for f in (sc.filters or []))
+    M, P = nu * np.asarray(Nu, dtype=float), my * np.asarray(N2, dtype=float)
+    per_step = 2 * (plant + model) + filt + 4 * my + 2 * nu * nx + 4 * my
+    return P * M * (M + 1) + M ** 3 / 3.0 + sc.nit * per_step
+
+
 def cpu_share():
     """(cpus, note): the CPUs this process may use -- its affinity set, limited by a cgroup CPU
     quota when one is set (the GPU box gives each GPU a share of the host)."""
@@ -577,14 +597,20 @@ def other_workload(args):
         fl = float(np.sum(nmpc_flops_per_sim(n_, u_, i_, nit=sc.nit)))
         kname, ibound = "nmpc_closed_loop_kernel (class launches)", "Gauss-Newton iterations"
     else:
-        # linear in the QP iterations: f(N2, Nu, 0) per horizon pair + 6 M^2 per iteration
-        fl = 0.0
-        for n, u in set(zip(cN2[live].tolist(), cNu[live].tolist())):
-            sel = (cN2[live] == n) & (cNu[live] == u)
-            fl += sel.sum() * algorithmic_flops_per_sim(sc, n, u, 0.0) + 6.0 * (sc.nu * u) ** 2 * i_[sel].sum()
         from mpct.engine import kernel_instance
 
-        kname, ibound = kernel_instance(sc), "QP iterations"
+        kname = kernel_instance(sc)
+        if kname.startswith("dtc_small_kernel"):
+            # the unconstrained DTC loop as computed: no QP, first-move rows only
+            fl = float(np.sum(dtc_flops_per_sim(sc, n_, u_)))
+            ibound = "the DTC loop's terms (no QP)"
+        else:
+            # linear in the QP iterations: f(N2, Nu, 0) per horizon pair + 6 M^2 per iteration
+            fl = 0.0
+            for n, u in set(zip(cN2[live].tolist(), cNu[live].tolist())):
+                sel = (cN2[live] == n) & (cNu[live] == u)
+                fl += sel.sum() * algorithmic_flops_per_sim(sc, n, u, 0.0) + 6.0 * (sc.nu * u) ** 2 * i_[sel].sum()
+            ibound = "QP iterations"
     achieved = fl / (kms * 1e-3) / 1e12
     # the PMC pass profiled one rank's whole grid: only a one-rank run evaluates the same launches
     traffic, traffic_source, fp64c = pmc_workload(args.workload, kms) if world == 1 else (

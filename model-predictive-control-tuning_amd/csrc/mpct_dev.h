@@ -202,6 +202,12 @@ enum { PROF_PROLOGUE = 0, PROF_PLANT, PROF_YUPD, PROF_UNC, PROF_QP, PROF_UUPD, P
 // prediction, the full-step (alpha = 1) trial prediction, the shorter Armijo trials (tangent-free),
 // the plant's RK4 step, everything else
 enum { PROF_NM_FULL = 0, PROF_NM_RINV, PROF_NM_QP, PROF_NM_AA, PROF_NM_LS0, PROF_NM_TRIAL, PROF_NM_PLANT,
-       PROF_NM_OTHER };
+       PROF_NM_OTHER, PROF_NM_NPASS, PROF_NM_POINTS, PROF_NM_USED, PROF_NM_ROWS };
+// counts only (tools/nmpc_fp64_split.py): PROF_NM_NPASS full passes (with
+// tangents), PROF_NM_POINTS the points they were asked for (the iterate, the Anderson candidate, the
+// alpha = 1 step, speculated first points of later calls), PROF_NM_USED the points whose
+// linearisation an iteration went on to use (the iterate's first pass, the accepted Anderson /
+// alpha = 1 point, a speculated point a later call started from), PROF_NM_ROWS the point rows each
+// pass occupies (G: four 16-lane rows in the M <= 15 class, one whole wave above)
 
 }  // namespace mpct

@@ -1219,7 +1219,8 @@ static int launch_batch(mpct_scenario* s, DevCtx* cx, int64_t C, const int32_t* 
                                   "qp.rotations", "qp.w.entry", "qp.w.rebuild", "qp.w.gather", "qp.w.solve",
                                   "qp.w.drop", "qp.w.rotations", "qp.w.readds"};
     const char* nmpc_nm[PROF_N] = {"full_pass", "rinv+step", "qp", "anderson_pass", "ls_full_pass", "ls_trials",
-                                   "plant_rk4", "other", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-", "-"};
+                                   "plant_rk4", "other", "n.passes", "n.points", "n.used", "n.rows", "-", "-", "-",
+                                   "-", "-", "-", "-", "-", "-"};
     const char** nm = s->nmpc ? nmpc_nm : gpc_nm;
     fprintf(stderr, "[mpct profile] mean / max cycles and mean executions per simulation over %lld sims\n", S);
     for (int k = 0; k < PROF_N; ++k)

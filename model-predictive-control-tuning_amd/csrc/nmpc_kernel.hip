@@ -394,12 +394,31 @@ __global__ void __launch_bounds__(64, 1)
         chf[k] = k < ndep ? fg[k + 1] : 0.0;
       }
     };
+#ifdef MPCT_PROFILE
+    if (cur >= 0) pacc[PROF_NM_USED] += kProfCount;  // a speculated first point, ready
+#define NM_COUNT_PASS(pts)                                         \
+  do {                                                             \
+    pacc[PROF_NM_NPASS] += kProfCount;                             \
+    pacc[PROF_NM_POINTS] += (unsigned long long)(pts) * kProfCount; \
+    pacc[PROF_NM_ROWS] += (unsigned long long)G * kProfCount;      \
+  } while (0)
+#define NM_COUNT_USED() pacc[PROF_NM_USED] += kProfCount
+#else
+#define NM_COUNT_PASS(pts) \
+  do {                     \
+  } while (0)
+#define NM_COUNT_USED() \
+  do {                  \
+  } while (0)
+#endif
     for (int it = 0; it < sc.sqp_max; ++it) {
       ++sqp_total;
       PSTAMP(PROF_NM_OTHER);
       if (cur < 0) {
         for (int g = 0; g < G; ++g) put(g, v);
         mpass(dchain, fg, xg);
+        NM_COUNT_PASS(1 + ndep);
+        NM_COUNT_USED();
         PSTAMP(PROF_NM_FULL);
         cur = 0;
         fcur = fg[0];
@@ -595,8 +614,10 @@ __global__ void __launch_bounds__(64, 1)
         // point from each on rows 2, 3
         const bool sp4 = G > 3 && nf > 0;
         mpass(sp4 ? 0x50u : 0u, fg, xg);
+        NM_COUNT_PASS((G > 1 ? 2 : 1) + (sp4 ? 2 : 0));
         PSTAMP(PROF_NM_AA);
         if (xg[0] && fg[0] <= f0 + kLsC1 * dd) {
+          NM_COUNT_USED();
           v = vc;
           cur = 0;
           fcur = fg[0];
@@ -607,6 +628,7 @@ __global__ void __launch_bounds__(64, 1)
         } else if (G > 1) {
           const double f1 = fg[1];
           if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
+            NM_COUNT_USED();
             v = va1;
             cur = 1;
             fcur = f1;
@@ -632,6 +654,7 @@ __global__ void __launch_bounds__(64, 1)
         if (ls == 0) {
           for (int g = 0; g < G; ++g) put(g, va);
           mpass(dchain, fg, xg);
+          NM_COUNT_PASS(1 + ndep);
           f1 = fg[0];
           PSTAMP(PROF_NM_LS0);
         } else {
@@ -640,6 +663,7 @@ __global__ void __launch_bounds__(64, 1)
         }
         if (f1 <= f0 + kLsC1 * alpha * dd || f1 - f0 <= kLsFlat * f0) {
           if (ls == 0) {
+            NM_COUNT_USED();
             cur = 0;
             fcur = f1;
             chain_of_solo();

@@ -63,6 +63,7 @@ class Scenario:
         # DTC-GPC (DTC_GPC_WW.m): GPC window, deltaUFree on the delays net of dmin (dnz)
         self.dtc = bool(dtc)
         self.nq = len(dist[0]) if dist else 0
+        self.dist, self.filters = dist, filters
         if self.dtc and window != "gpc":
             raise ValueError("DTC mode uses the GPC window (MatG/diophantine N1 = dmin+1)")
         dp_desc = (dp - self.dmin[:, None]) if self.dtc else dp
