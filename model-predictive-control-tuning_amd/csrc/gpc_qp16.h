@@ -60,7 +60,11 @@ constexpr int kBS = 16;
 // and on the heaviest 256: both add live values to a step loop at the 128-VGPR budget, whose
 // allocator answers with 2-5 more step-loop invariants spilled and reloaded every step.  The same
 // R_A(jj, jj) by readlane alone (loaded one rotation ahead otherwise) was 1-4 % slower as well,
-// with or without the bounds in LDS (profiles/r06c_metric_ab.txt)
+// with or without the bounds in LDS (profiles/r06c_metric_ab.txt).  Once the bounds in LDS freed
+// nine VGPRs, the chain without per-rotation hand-offs (fence only), with R_A(jj, jj) by readlane,
+// and with R_A's row and B's column carried in registers fit without a spill, and none was faster
+// (bitwise equal, within 1 % either way, profiles/r06f_drop_chain_ab.txt): the heaviest
+// simulations' drops are not on a chain the hand-offs lengthen
 
 // the lane id as an opaque value, re-derived at every use: the step loop's register budget cannot
 // hold the dozens of lane-derived addresses and predicates the compiler would otherwise hoist out
