@@ -65,11 +65,16 @@ __device__ __forceinline__ int dtc_lane() {
   return l;
 }
 
-// waves per SIMD the launch bounds ask for: the <16> instance needs 119 VGPRs unbounded (four
-// waves); five waves (96 VGPRs, 80 B of prologue spill) measured 21.2 against 22.8 ms for config
-// 4's 320,000 simulations, six (80 VGPRs) 21.7 ms (profiles/r06d_dtc_small_ab.txt)
+// waves per SIMD the launch bounds ask for, and the prologue's Householder block (gpc_prologue.h
+// kHB): unbounded the <16> instance needs 119 VGPRs (four waves; 22.9 ms for config 4's 320,000
+// simulations); five waves with 8-row blocks spill 80 B per lane in the prologue (21.3 ms, but 1.33 GB
+// of scratch write-backs per evaluation against 10 MB of records); four waves with 4-row blocks fit
+// 103 VGPRs without a spill: 21.5 ms and 10.2 MB written (profiles/r06i_dtc_prologue_ab.txt)
+#ifndef MPCT_DTC_HB
+#define MPCT_DTC_HB 4
+#endif
 #ifndef MPCT_DTC_W16
-#define MPCT_DTC_W16 5
+#define MPCT_DTC_W16 4
 #endif
 #ifndef MPCT_DTC_W32
 #define MPCT_DTC_W32 3
@@ -115,7 +120,7 @@ __global__ void __launch_bounds__(64, MAXM <= 16 ? MPCT_DTC_W16 : MPCT_DTC_W32)
 
   // ------------------------------------------------------------------ prologue (gpc_prologue.h):
   // the first-move rows of A only (row n = A row n Nu), no R^-1
-  if (!gpc_prologue<MAXM, false, false, true>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.R,
+  if (!gpc_prologue<MAXM, false, false, true, MPCT_DTC_HB>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.R,
                                               nullptr, lds + L.A, kSmA, sc.sm_acol)) {
     write_nan(MPCT_ST_NONFINITE_);
     return;

@@ -24,12 +24,11 @@ namespace mpct {
 // nullptr = identity).  Returns false (uniformly) when R is not positive definite.
 // RINV = false: no R^-1 (an unconstrained loop has no QP); FIRST = true: only the first-move rows
 // m = n Nu of A, stored as row n (DTC_GPC_WW.m:105 Km: the unconstrained loop applies those alone)
-template <int MAXM, bool PACKED = false, bool RINV = true, bool FIRST = false>
+template <int MAXM, bool PACKED = false, bool RINV = true, bool FIRST = false, int kHB = 8>
 __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, int M, int Nu, int N2,
                                              const double* dl, const double* lm, double* sR, double* sRi,
                                              double* sA, int astride, const int* acol) {
   const int my = sc.my, nu = sc.nu, nx = sc.nx;
-  constexpr int kHB = 8;
   const int vper = kWave - M;  // V columns per pass (host guarantees M < 64)
   const int npass = (nx + vper - 1) / vper;
   double rcol[MAXM];

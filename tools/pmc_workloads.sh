@@ -20,7 +20,7 @@ done
 python3 - "$O" "$SHA" "$T" <<'PY'
 import collections, csv, glob, json, sys
 O, sha, tag = sys.argv[1], sys.argv[2], sys.argv[3]
-fam = {"shell7x5": "mdband_closed_loop", "vandevusse": "nmpc_closed_loop", "dtc-mc": "gpc_closed_loop"}
+fam = {"shell7x5": "mdband_closed_loop", "vandevusse": "nmpc_closed_loop", "dtc-mc": "dtc_small_kernel"}  # r06: config 4 runs dtc_small_kernel
 EVALS = 2  # --warmup 1 --steps 1
 rep = {"lib_sha256": sha, "tag": tag, "evaluations_profiled": EVALS,
        "units": "per evaluation of the workload's grid (one bench.py step), summed over the kernel family's "

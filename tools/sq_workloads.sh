@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the three other workloads: config 3 (mdband_closed_loop_kernel,
 # tools/bench_config3.py), config 5 (nmpc_closed_loop_kernel, tools/bench_config5.py) and config 4
-# (the DTC instances of gpc_closed_loop_kernel, tools/bench_dtc_mc.py).  Per workload: two SQ passes
+# (config 4: dtc_small_kernel since round 6, tools/bench_dtc_mc.py).  Per workload: two SQ passes
 # (issue, waits, FP64 mix, LDS bank conflicts) and separate FETCH_SIZE / WRITE_SIZE passes, each its
 # own rocprofv3 run, kernel-trace only, under its own time limit.  Summary (sums over the timed
 # dispatches of the workload's kernel family): gpurun_out/sqw/summary.json
@@ -22,7 +22,7 @@ run config4 python3 $R/tools/bench_dtc_mc.py
 python3 - "$O" "$(sha256sum $R/model-predictive-control-tuning_amd/csrc/libmpct.so | cut -c1-64)" <<'PY'
 import collections, csv, glob, json, sys
 O, sha = sys.argv[1], sys.argv[2]
-fam = {"config3": "mdband_closed_loop", "config5": "nmpc_closed_loop", "config4": "gpc_closed_loop"}
+fam = {"config3": "mdband_closed_loop", "config5": "nmpc_closed_loop", "config4": "dtc_small_kernel"}  # r06: config 4 runs dtc_small_kernel
 rep = {"lib_sha256": sha, "units": "sums over every dispatch of the kernel family in one run of the workload; "
        "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles; FETCH_SIZE / WRITE_SIZE in KiB (hbm_*_bytes corrected)"}
 for w, k in fam.items():
