@@ -148,7 +148,7 @@ def cell_halves(idx, work):
 SHARD_OVERLAP = 0.54
 # cells costlier than this are split into their two halves before packing (None: an even share,
 # total / world).  Splitting measured no better: a half's alone-time is most of its cell's (the
-# heaviest cell 129 ms whole, 119 + 93 ms as halves; r06a_config3_cells.json), so halves add load
+# heaviest cell 129 ms whole, 119 + 93 ms as halves; mpct/config3_cells.json, profiles/r06a_shard_balance.json), so halves add load
 SPLIT_MS = None
 
 

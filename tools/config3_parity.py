@@ -5,7 +5,7 @@ Writes a JSON report: the fraction of candidates whose J1 (stratified 8,192, per
 J1 @ SHELL7_W (whole grid) differs by more than 1e-6 relative, the top-64 ranking check, and for
 the divergent candidates of the sample: the per-step replay (oracle first move at the state the
 device reached, all 200 steps) and the first step at which the device's free run leaves the
-C port's free run.  Usage: python tools/config3_parity.py --out profiles/r03_config3_parity.json"""
+C port's free run.  Usage: python tools/config3_parity.py --out gpurun_out/config3_parity.json (committed runs: profiles/r03b_config3_parity_tol_*.json)"""
 import argparse
 import json
 import os
