@@ -48,7 +48,10 @@ struct RegFactors {
 // B's row stride.  Stride 16 has the column writes of an add 16-way, the drop's column reads 8-way
 // and b_row4's row reads 4-way in LDS bank conflict (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 // 18.6 %); stride 18 halves that (13.7 %) but measured no faster, 1-2 % slower at 1024 and 8192
-// candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain
+// candidates (profiles/r03n_bs_stride_ab.txt): the conflicts are not on the chain.  Round 6 rotated each
+// row's 4-double blocks by (i >> 1) & 3 instead, and A's row reads in gpc_small.hip: conflicts 19.4 ->
+// 7.4 % of LDS cycles, kernel 3-4 % slower (the index arithmetic sits on the QP chain; the A rotation
+// alone was within noise), profiles/r06m_lds_banks_ab.txt
 constexpr int kBS = 16;
 
 // Drops keep R_A and its Givens chain: drops derived from B alone, as the band kernel's (DESIGN §11

@@ -813,10 +813,12 @@ __global__ void __launch_bounds__(64, 1)
 namespace mpct {
 
 
-// LDS tiers (KB) of the class launches.  One wave per SIMD (342 / 418 VGPRs), so at most four
-// workgroups per CU: the M <= 15 class sizes its point buffers to 40 KB (nm_groups), one tier;
-// the M <= 32 class 32 KB, the rest above (finer tiers measured slower)
-constexpr long long kNmCap16Kb = 40, kNmCap32Kb = 32;
+// LDS tiers (KB) of the class launches.  One wave per SIMD (396 / 412 VGPRs), so at most four
+// workgroups per CU, which 40 KB still allows: the M <= 15 class sizes its point buffers to 40 KB
+// (nm_groups), one tier; the M <= 32 class 40 KB, the rest above (a 32 KB first tier held the
+// simulations between 32 and 40 KB to three per CU: config 5 21.7 k -> 22.0-22.3 k sims/s at 40,
+// profiles/r06m_lds_banks_ab.txt; finer tiers measured slower)
+constexpr long long kNmCap16Kb = 40, kNmCap32Kb = 40;
 
 long long nmpc_lds_bytes(int M, int N) { return (long long)nm_layout(M, N, nm_groups(M, N)).total * 8; }
 

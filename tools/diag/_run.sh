@@ -1,12 +1,18 @@
 #!/bin/bash
-# end-of-round keyed pass: the workload PMC pass and the four bench lines read back against the committed
-# metric PMC / latency model (tools/diag/_keyed.sh), the 8-rank config-3 plans on one GPU, and the
-# 400-iteration Van de Vusse tuning run
-set -eo pipefail
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06k}; O="$R/gpurun_out/$T"; mkdir -p "$O"
-bash tools/diag/_keyed.sh $T
-timeout -k 10 400 python3 tools/shard_balance.py --only shell7x5 --plans 0.54:none --out "$O/shard_plans.json" \
-  > "$O/shard_plans.log" 2>&1 || { tail -20 "$O/shard_plans.log"; exit 1; }
-timeout -k 10 300 python3 tools/tune_vandevusse.py "$O/vdv_tuning.mat" > "$O/tune_vandevusse.log" 2>&1 \
-  || { tail -20 "$O/tune_vandevusse.log"; exit 1; }
-echo all done
+# r06m: metric LDS bank variants (A-row rotation, B block swizzle, both) A/B against the release library:
+# three interleaved qab rounds with bitwise dumps, one LDS PMC pass each; the metric parity tests on
+# the combined build; the NMPC tests on the 40 KB-tier build
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06m}; O="gpurun_out/$T"; mkdir -p "$O"
+C=$R/model-predictive-control-tuning_amd/csrc
+AB=()
+for rep in 1 2 3; do
+  for v in base arot bswz ba; do
+    AB+=("45 ab_${v}_$rep env MPCT_LIB=$C/libmpct_$v.so QAB_DUMP=$O/ab_$v.npz python3 tools/qab.py h256 4096 8192")
+  done
+done
+for v in base arot bswz ba; do
+  AB+=("90 lds_$v export TMPDIR=/tmp; MPCT_LIB=$C/libmpct_$v.so timeout -s KILL 80 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES --output-format csv -d $O/lds_$v -o p -- python3 tools/qab.py 4096")
+done
+AB+=("300 par_ba env MPCT_LIB=$C/libmpct_ba.so python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread")
+AB+=("300 nm_cap40 env MPCT_LIB=$C/libmpct_cap40.so python3 -u -m pytest tests/test_nmpc.py -m gpu -x -q --timeout 240 --timeout-method thread")
+bash tools/gpu_steps.sh "$O" "${AB[@]}"
