@@ -359,8 +359,11 @@ __global__ void __launch_bounds__(64, 1)
 #pragma unroll
         for (int k = 0; k < MAXM; ++k)
           if (k < M) {
-            if (prow) gR[k * M + gl] = rcol[k];
-            else gc[k] = rcol[k];
+            if (prow) {
+              if (k <= gl) gR[nm_up(k, gl, M)] = rcol[k];
+            } else {
+              gc[k] = rcol[k];
+            }
           }
       }
       const double rv2 = prow ? (pwu * va) * (pwu * va) : 0.0;
@@ -427,20 +430,19 @@ __global__ void __launch_bounds__(64, 1)
       setcur(cur);
       const double f0 = fcur;
       lds_sync();
-      // R^-1 (upper, row-major): lane j solves R x = e_j in its own column
+      // R^-1 (upper, packed by rows): lane j solves R x = e_j in its own column
       if (row) {
         for (int kk = lane; kk >= 0; --kk) {
           double a = (kk == lane) ? 1.0 : 0.0;
-          for (int j = kk + 1; j <= lane; ++j) a -= sR[kk * M + j] * sRi[j * M + lane];
-          sRi[kk * M + lane] = a / sR[kk * M + kk];
+          for (int j = kk + 1; j <= lane; ++j) a -= sR[nm_up(kk, j, M)] * sRi[nm_up(j, lane, M)];
+          sRi[nm_up(kk, lane, M)] = a / sR[nm_up(kk, kk, M)];
         }
-        for (int kk = lane + 1; kk < M; ++kk) sRi[kk * M + lane] = 0.0;
       }
       lds_sync();
       // unconstrained Gauss-Newton step s_u = -R^-1 c
       double xm = 0.0;
       if (row)
-        for (int k = lane; k < M; ++k) xm -= sRi[lane * M + k] * scv[k];
+        for (int k = lane; k < M; ++k) xm -= sRi[nm_up(lane, k, M)] * scv[k];
       PSTAMP(PROF_NM_RINV);
       // ---- box QP: lb <= U + cumulative step <= ub, Goldfarb-Idnani from s_u
       const double clo = row ? lbn - sU[lane] : 0.0, chi = row ? ubn - sU[lane] : 0.0;
@@ -448,7 +450,13 @@ __global__ void __launch_bounds__(64, 1)
       GIState<MAXM> gis;
       gi_reset<MAXM>(gis);
       for (int w = lane; w < nbits; w += kWave) sbits[w] = 0u;
-      gi_load_rinv<MAXM>(gis, sJT, sRi, M, row);
+      // J = R^-1 (gi_core's J'-in-LDS layout, sJT[k M + i] = J(i, k)) from the packed upper triangle
+      if (row)
+#pragma unroll 1
+        for (int k = 0; k < M; ++k) sJT[k * M + lane] = k >= lane ? sRi[nm_up(lane, k, M)] : 0.0;
+      gis.nrot = 0;
+      gis.jinit = true;
+      lds_sync();
       const StateMark mark{sbits, 4 * M};
       int git = 0;
       for (;;) {
@@ -507,7 +515,7 @@ __global__ void __launch_bounds__(64, 1)
           const double dn2 = qsum<MAXM>(d2);
           const double beta = qsum<MAXM>(lane >= gis.q ? d2 : 0.0);
           const double zm = gi_z(sJT, sd, gis.q, M, row);
-          const double rk = gi_backsub<MAXM>(gis, sRA, M, dk);
+          const double rk = gi_backsub<MAXM>(gis, sRA, M, dk, RAPacked{});
           double t1 = INFINITY;
           int kdrop = 0x7fffffff;
           if (lane < gis.q && rk > 0.0) {
@@ -528,7 +536,7 @@ __global__ void __launch_bounds__(64, 1)
           upm += t;
           sp += t * beta;
           if (full) {
-            gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, mark);
+            gi_add<MAXM>(gis, sJT, sRA, sd, M, p, dk, beta, zm, upm, row, mark, RAPacked{});
             break;
           }
           if (kdrop >= gis.q) {  // t1 or t2 NaN: no lane attains the ratio test (a non-finite state)
@@ -536,7 +544,7 @@ __global__ void __launch_bounds__(64, 1)
             infeas = true;
             break;
           }
-          gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, mark);
+          gi_drop<MAXM>(gis, sJT, sRA, M, kdrop, mark, RAPacked{});
           if (git >= maxit) break;
         }
         if (infeas) break;
@@ -569,7 +577,7 @@ __global__ void __launch_bounds__(64, 1)
       lds_sync();
       double rs = 0.0;
       if (row)
-        for (int j = lane; j < M; ++j) rs += sR[lane * M + j] * sxc[j];
+        for (int j = lane; j < M; ++j) rs += sR[nm_up(lane, j, M)] * sxc[j];
       const double dd = qsum<MAXM>(row ? scv[lane] * rs : 0.0);
       // ---- Anderson step (oracle/nmpc_vdv.py AA_DEPTH = 1): gamma = <df, d>/<df, df> on the
       // absolute moves scaled by 1/s_u, candidate clip(G(v) - gamma (G(v) - G(v'))); taken when
@@ -813,7 +821,7 @@ __global__ void __launch_bounds__(64, 1)
 namespace mpct {
 
 
-// LDS tiers (KB) of the class launches.  One wave per SIMD (396 / 412 VGPRs), so at most four
+// LDS tiers (KB) of the class launches.  One wave per SIMD (384 / 434 VGPRs), so at most four
 // workgroups per CU, which 40 KB still allows: the M <= 15 class sizes its point buffers to 40 KB
 // (nm_groups), one tier; the M <= 32 class 40 KB, the rest above (a 32 KB first tier held the
 // simulations between 32 and 40 KB to three per CU: config 5 21.7 k -> 22.0-22.3 k sims/s at 40,

@@ -45,6 +45,9 @@ __device__ __forceinline__ void vdv_rhs(const VdV& P, const double x[3], const d
   // 1/th by v_rcp_f64 + two Newton steps (config 5: 326 -> 293 ms, profiles/r02i_nmpc_rhs_ab.txt);
   // an Estrin-scheme exp measured 306 ms (more VALU than the libm exp) and is not kept
   const double ith = rcp_nr(th);
+  // a table-driven exp (16 entries of 2^(j/16) in LDS, degree-7 expm1, within 1 ulp) took fewer
+  // instructions than the library's but measured slower, config 5 24.1 -> 23.5 k sims/s and the N = 31
+  // loop 30.2 -> 31.2 ms: its LDS load sits on the stage's chain (profiles/r06p_nmpc_ab.txt)
   const double ex1 = exp(P.e1 * ith);
   const double k1 = P.k10 * ex1;
   const double k2 = P.k20 * (P.e2 == P.e1 ? ex1 : exp(P.e2 * ith));  // E1 = E2 in the reference model
@@ -119,9 +122,9 @@ __host__ __device__ inline NmLayout nm_layout(int M, int N, int G) {
   NmLayout L;
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
-  L.ri = take(M * M);
+  L.ri = take(M * (M + 1) / 2);  // R^-1, upper triangle packed by rows (nm_up)
   L.jt = take(M * M);
-  L.ra = take(M * M);
+  L.ra = take((M * (M + 3)) / 2);  // R_A, packed upper Hessenberg (gi_core.h RAPacked, ra_packed_size)
   L.dv = take(M + 1);
   L.xc = take(M + 1);
   L.uo = take(M + 1);  // absolute moves of the open-loop solution (Info.MVopt)
@@ -130,7 +133,7 @@ __host__ __device__ inline NmLayout nm_layout(int M, int N, int G) {
   const int w = G > 1 ? 16 : M + 1;  // per-lane vectors of a point (16-lane rows when grouped)
   int g = 0;
   auto gtake = [&](int n) { int r = g; g += (n + 1) & ~1; return r; };
-  L.g_rr = gtake(M * M);  // R of the Gauss-Newton least-squares QR (row-major, upper)
+  L.g_rr = gtake(M * (M + 1) / 2);  // R of the Gauss-Newton least-squares QR (upper, packed: nm_up)
   L.g_cv = gtake(w);
   L.g_u = gtake(w);
   L.g_v = gtake(w);
@@ -143,6 +146,11 @@ __host__ __device__ inline NmLayout nm_layout(int M, int N, int G) {
   L.total = (o + 1) & ~1;
   return L;
 }
+
+// entry (i, k), k >= i, of an upper-triangular M x M matrix packed row by row: R and R^-1 keep only
+// their upper triangles (round 6: 3.4 KB less at M = 15 with four point buffers, 7 KB at M = 30, so
+// more simulations fit the 40 KB of four workgroups per CU; the lower entries were never read)
+__host__ __device__ inline int nm_up(int i, int k, int M) { return i * M - ((i * (i - 1)) >> 1) + (k - i); }
 
 // point buffers of a simulation: four (one per 16-lane row) when they fit 40 KB, i.e. four
 // workgroups per CU, the one-wave-per-SIMD occupancy of this kernel; else two while they fit the
