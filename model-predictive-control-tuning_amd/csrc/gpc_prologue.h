@@ -123,10 +123,14 @@ __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, in
     }
     if (pass == 0) {  // R to LDS; singular R -> status
       lds_sync();
-      if (lane < M) {
+      // the lane id through an opaque copy: otherwise the compiler forms the M store addresses
+      // before the QR and keeps them live across it, where a 12-row block spills them (round 6)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      if (ln < M) {
 #pragma unroll
         for (int k = 0; k < MAXM; ++k)
-          if (k < M) sR[k * M + lane] = rcol[k];
+          if (k < M) sR[k * M + ln] = rcol[k];
       }
       lds_sync();
       bool spd = true;

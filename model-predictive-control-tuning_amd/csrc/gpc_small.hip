@@ -115,7 +115,10 @@ __global__ void __launch_bounds__(64, 4)
   lds_sync();
 
   // ------------------------------------------------------------------ prologue (gpc_prologue.h)
-  if (!gpc_prologue<16, true>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.ra, lds + L.rinv,
+  // Householder blocks of 12 rows (round 6: 8 before; 12 fits 121 VGPRs once the R-store addresses
+  // stop being hoisted across the QR, gpc_prologue.h): the heaviest 256 1.78-1.79 -> 1.76 ms, 8192
+  // candidates 2.85 -> 2.78 ms, J1 within 1.8e-10 of the 8-row blocks (profiles/r06t_prologue_ab.txt)
+  if (!gpc_prologue<16, true, true, false, 12>(sc, lane, M, Nu, N2, deltav + c * my, lambdav + c * nu, lds + L.ra, lds + L.rinv,
                               sA, kSmA, sc.sm_acol)) {
     write_nan(MPCT_ST_NONFINITE_);
     return;
