@@ -1,12 +1,17 @@
 #!/bin/bash
-# end-of-round keyed pass: the workload PMC pass and the four bench lines read back against the committed
-# metric PMC / latency model (tools/diag/_keyed.sh), the 8-rank config-3 plans on one GPU, and the
-# 400-iteration Van de Vusse tuning run
-set -eo pipefail
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06w}; O="$R/gpurun_out/$T"; mkdir -p "$O"
-bash tools/diag/_keyed.sh $T
-timeout -k 10 400 python3 tools/shard_balance.py --only shell7x5 --plans 0.54:none --out "$O/shard_plans.json" \
-  > "$O/shard_plans.log" 2>&1 || { tail -20 "$O/shard_plans.log"; exit 1; }
-timeout -k 10 300 python3 tools/tune_vandevusse.py "$O/vdv_tuning.mat" > "$O/tune_vandevusse.log" 2>&1 \
-  || { tail -20 "$O/tune_vandevusse.log"; exit 1; }
-echo all done
+# r06x: NMPC streamed QR with both output rows in flight (qr2, -DMPCT_NM_QR2) against the release (base,
+# 628c0cd4) and the same source without it (ref): config-5 bench, three interleaved rounds, the small-batch
+# latency, and the NMPC GPU tests on qr2
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06x}; O="gpurun_out/$T"; mkdir -p "$O"
+C=$R/model-predictive-control-tuning_amd/csrc
+AB=()
+for rep in 1 2 3; do
+  for v in base ref qr2; do
+    AB+=("120 c5_${v}_$rep env MPCT_LIB=$C/libmpct_$v.so python3 bench.py --workload vandevusse --steps 3 --warmup 1 --no-cpu-baseline")
+  done
+done
+for v in base qr2; do
+  AB+=("120 lat_$v env MPCT_LIB=$C/libmpct_$v.so python3 tools/nmpc_latency.py")
+done
+AB+=("400 nm_qr2 env MPCT_LIB=$C/libmpct_qr2.so python3 -u -m pytest tests/test_nmpc.py -m gpu -x -q --timeout 300 --timeout-method thread")
+bash tools/gpu_steps.sh "$O" "${AB[@]}"
