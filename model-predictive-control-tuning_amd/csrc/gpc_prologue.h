@@ -101,8 +101,12 @@ __device__ __forceinline__ bool gpc_prologue(const DevScenario& sc, int lane, in
       const double f = beta * (s0 + s1);
       const bool own = lane == k;
       rcol[k] = own ? n : fma(-f, v0, rcol[k]);
+      // lane k keeps its block entries' rounding residue instead of an exact 0: they only ever reach
+      // lanes left of later pivots, i.e. R's lower triangle, which nothing reads, so R's upper
+      // triangle and T are bitwise those of the select (round 6: 24 v_cndmask fewer per reflection,
+      // the metric 1 % faster, profiles/r06z_prologue_nosel_ab.txt)
 #pragma unroll
-      for (int i = 0; i < kHB; ++i) w[i] = own ? 0.0 : fma(-f, wk[i], w[i]);
+      for (int i = 0; i < kHB; ++i) w[i] = fma(-f, wk[i], w[i]);
     };
     const int P = my * N2;
     const int nblk = (P + kHB - 1) / kHB;
