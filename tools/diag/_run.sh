@@ -1,12 +1,14 @@
 #!/bin/bash
-# r06aa: the GPU suite on the no-select prologue build (8a6d257b), then config 4 with dtc_small_kernel's prologue
-# blocks of 4 (release), 8 and 12 rows, three interleaved bench rounds
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06aa}; O="gpurun_out/$T"; mkdir -p "$O"
-C=$R/model-predictive-control-tuning_amd/csrc
-AB=("600 pytest python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread")
-for rep in 1 2 3; do
-  for v in base dh8 dh12; do
-    AB+=("120 c4_${v}_$rep env MPCT_LIB=$C/libmpct_$v.so python3 bench.py --workload dtc-mc --steps 5 --warmup 2 --no-cpu-baseline")
-  done
-done
-bash tools/gpu_steps.sh "$O" "${AB[@]}"
+# end-of-round evidence pass: tools/gpu_evidence.sh (GPU suite, smoke, metric bench line, kernel
+# trace, FETCH_SIZE / WRITE_SIZE and two SQ passes of the metric), the latency probe, the
+# heaviest-256 section profile of the -DMPCT_PROFILE build, the SQ counters of the heaviest 256, and
+# every workload's bench line with a kernel trace each
+set -eo pipefail
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06ab}; O="$R/gpurun_out/$T"; mkdir -p "$O"
+bash tools/gpu_evidence.sh $T
+timeout -k 10 60 tools/latency_probe > "$O/probe.json"
+MPCT_PROF_OUT="$O/prof_heavy256.bin" timeout -k 10 120 python3 tools/kprof.py 256 heavy > "$O/kprof.txt" 2>&1
+bash tools/sq_heavy.sh
+cp gpurun_out/sqh/summary.json "$O/sq_heavy.json"
+bash tools/gpu_bench_all.sh ${T}_all > "$O/bench_all.log" 2>&1
+echo all done
