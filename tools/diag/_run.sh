@@ -1,12 +1,8 @@
 #!/bin/bash
-# end-of-round keyed pass: the workload PMC pass and the four bench lines read back against the committed
-# metric PMC / latency model (tools/diag/_keyed.sh), the 8-rank config-3 plans on one GPU, and the
-# 400-iteration Van de Vusse tuning run
-set -eo pipefail
-R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06ac}; O="$R/gpurun_out/$T"; mkdir -p "$O"
-bash tools/diag/_keyed.sh $T
-timeout -k 10 400 python3 tools/shard_balance.py --only shell7x5 --plans 0.54:none --out "$O/shard_plans.json" \
-  > "$O/shard_plans.log" 2>&1 || { tail -20 "$O/shard_plans.log"; exit 1; }
-timeout -k 10 300 python3 tools/tune_vandevusse.py "$O/vdv_tuning.mat" > "$O/tune_vandevusse.log" 2>&1 \
-  || { tail -20 "$O/tune_vandevusse.log"; exit 1; }
-echo all done
+# r06ad (diagnostic): the metric QP's drops split into setup + shifts (the open_loop slot of the profile build,
+# unused by the metric) and rotations, over the heaviest 256 simulations; the plain profile build beside it
+R="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$R"; T=${1:-r06ad}; O="gpurun_out/$T"; mkdir -p "$O"
+C=$R/model-predictive-control-tuning_amd/csrc
+bash tools/gpu_steps.sh "$O" \
+  "120 kprof_ds env MPCT_LIB=$C/libmpct_profds.so MPCT_PROF_OUT=$O/ds.bin python3 tools/kprof.py 256 heavy" \
+  "120 kprof env MPCT_LIB=$C/libmpct_prof.so MPCT_PROF_OUT=$O/base.bin python3 tools/kprof.py 256 heavy"
